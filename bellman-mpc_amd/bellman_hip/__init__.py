@@ -1,0 +1,538 @@
+"""bellman_hip -- Python host layer over the MI355X Groth16 prover core.
+
+Mirrors the reference crate's API for the hot path (paths relative to
+/root/reference/bellman/src):
+
+  multiexp(ctx, bases, offset, density, exponents)   multiexp.rs:252-281
+  EvaluationDomain.{fft, ifft, coset_fft, ...}        domain.rs:42-190
+  Parameters.read / .write                            groth16/mod.rs:260-400
+  ProvingAssignment / create_proof / create_random_proof
+                                                       groth16/prover.rs:19-350
+  Circuit / ConstraintSystem / LinearCombination      lib.rs:203-623
+
+All arithmetic runs in libbellman_hip.so (HIP kernels for gfx950) through the
+C ABI declared in include/bellman_hip.h; this module only marshals.  If the
+shared library is missing this module raises at import time -- there is no
+CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libbellman_hip.so")
+
+R_MODULUS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+_MONT_R = pow(2, 256, R_MODULUS)
+_MONT_RINV = pow(_MONT_R, -1, R_MODULUS)
+
+BH_OK = 0
+BH_G1, BH_G2 = 1, 2
+BH_SCALARS_CANONICAL, BH_SCALARS_MONTGOMERY = 0, 1
+
+
+class SynthesisError(Exception):
+    """Mirrors lib.rs:355-364; .code is the bh_status."""
+
+    def __init__(self, code, msg=""):
+        super().__init__(f"{msg} (status {code}: {_status_string(code)})")
+        self.code = code
+
+
+class UnexpectedIdentity(SynthesisError):
+    pass
+
+
+class UnexpectedEof(SynthesisError):
+    pass
+
+
+class PolynomialDegreeTooLarge(SynthesisError):
+    pass
+
+
+class DensitySizeMismatch(SynthesisError):
+    pass
+
+
+class AssignmentMissing(SynthesisError):
+    def __init__(self):
+        super().__init__(6, "assignment missing")
+
+
+_ERRS = {1: UnexpectedIdentity, 2: UnexpectedEof, 3: PolynomialDegreeTooLarge, 4: DensitySizeMismatch}
+
+
+def _load():
+    if not os.path.exists(_LIB_PATH):
+        raise ImportError(f"bellman_hip: {_LIB_PATH} not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_LIB_PATH)
+    P, S, U64, I, U8 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32
+    sig = {
+        "bh_status_string": (ctypes.c_char_p, [I]),
+        "bh_version": (I, []),
+        "bh_ctx_create": (I, [I, P]),
+        "bh_ctx_destroy": (I, [P]),
+        "bh_ctx_reserve": (I, [P, S, U8]),
+        "bh_ctx_set_window": (I, [P, I]),
+        "bh_srs_upload": (I, [P, I, P, S, I, P]),
+        "bh_srs_free": (I, [P]),
+        "bh_srs_len": (S, [P]),
+        "bh_srs_get": (I, [P, S, P]),
+        "bh_multiexp": (I, [P, P, S, P, S, P, S, I, P]),
+        "bh_domain_size": (I, [S, P, P]),
+        "bh_fft": (I, [P, P, U8]),
+        "bh_ifft": (I, [P, P, U8]),
+        "bh_coset_fft": (I, [P, P, U8]),
+        "bh_icoset_fft": (I, [P, P, U8]),
+        "bh_distribute_powers": (I, [P, P, S, P]),
+        "bh_divide_by_z_on_coset": (I, [P, P, U8]),
+        "bh_mul_assign": (I, [P, P, P, S]),
+        "bh_sub_assign": (I, [P, P, P, S]),
+        "bh_compute_h": (I, [P, P, P, P, S, P, P]),
+        "bh_params_load": (I, [P, P, S, I, P]),
+        "bh_params_free": (I, [P]),
+        "bh_params_sizes": (I, [P, P]),
+        "bh_params_write": (I, [P, P, S, P]),
+        "bh_prove": (I, [P, P, P, P, P, S, P, S, P, S, P, P, P, P, P, P]),
+        "bh_witness_upload": (I, [P, P, P, P, S, P, S, P, S, P, P, P, P]),
+        "bh_witness_free": (I, [P]),
+        "bh_prove_witness": (I, [P, P, P, P, P, P]),
+        "bh_chain_witness": (I, [P, S, U64, P]),
+        "bh_chain_params": (I, [P, S, U64, U64, U64, U64, U64, U64, P]),
+        "bh_last_timings": (I, [P, P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+# every symbol declared in include/bellman_hip.h
+EXPORTED_SYMBOLS = [
+    "bh_status_string", "bh_version", "bh_ctx_create", "bh_ctx_destroy", "bh_ctx_reserve", "bh_ctx_set_window",
+    "bh_srs_upload", "bh_srs_free", "bh_srs_len", "bh_srs_get", "bh_multiexp", "bh_domain_size", "bh_fft",
+    "bh_ifft", "bh_coset_fft", "bh_icoset_fft", "bh_distribute_powers", "bh_divide_by_z_on_coset",
+    "bh_mul_assign", "bh_sub_assign", "bh_compute_h", "bh_params_load", "bh_params_free", "bh_params_sizes",
+    "bh_prove", "bh_witness_upload", "bh_witness_free", "bh_prove_witness", "bh_chain_witness",
+    "bh_chain_params", "bh_params_write", "bh_last_timings",
+]
+
+
+def lib():
+    return _lib
+
+
+def _status_string(code):
+    s = _lib.bh_status_string(int(code))
+    return s.decode() if s else "?"
+
+
+def _check(code, what=""):
+    if code != BH_OK:
+        raise _ERRS.get(code, SynthesisError)(code, what)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ------------------------------------------------------------------ Fr encodings
+def fr_to_mont(values):
+    """ints -> (n,4) uint64 bls12_381 Montgomery limbs."""
+    out = np.zeros((len(values), 4), dtype=np.uint64)
+    for i, v in enumerate(values):
+        x = (int(v) % R_MODULUS) * _MONT_R % R_MODULUS
+        out[i] = [(x >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)]
+    return out
+
+
+def fr_from_mont(arr):
+    out = []
+    for row in np.asarray(arr, dtype=np.uint64).reshape(-1, 4):
+        x = sum(int(row[k]) << (64 * k) for k in range(4))
+        out.append(x * _MONT_RINV % R_MODULUS)
+    return out
+
+
+def fr_to_canonical_limbs(values):
+    """ints -> (n,4) uint64 canonical (Scalar::to_le_bits words)."""
+    out = np.zeros((len(values), 4), dtype=np.uint64)
+    for i, v in enumerate(values):
+        x = int(v) % R_MODULUS
+        out[i] = [(x >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)]
+    return out
+
+
+def density_words(bits):
+    """list[bool] -> uint64 words (bitvec Lsb0)."""
+    n = len(bits)
+    w = np.zeros(max(1, (n + 63) // 64), dtype=np.uint64)
+    for i, b in enumerate(bits):
+        if b:
+            w[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
+    return w
+
+
+# ------------------------------------------------------------------ context / bases
+class Context:
+    """One MI355X device: streams + workspaces (replaces multicore::Worker)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _check(_lib.bh_ctx_create(device, ctypes.byref(h)), "bh_ctx_create")
+        self.h = h
+
+    def reserve(self, max_msm_len, max_log_domain=0):
+        _check(_lib.bh_ctx_reserve(self.h, max_msm_len, max_log_domain), "bh_ctx_reserve")
+
+    def set_window(self, c):
+        _check(_lib.bh_ctx_set_window(self.h, c), "bh_ctx_set_window")
+
+    def last_timings(self):
+        out = (ctypes.c_double * 8)()
+        _check(_lib.bh_last_timings(self.h, out))
+        return list(out)
+
+    def close(self):
+        if self.h:
+            _lib.bh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Bases:
+    """Device-resident Arc<Vec<G1Affine|G2Affine>> (the multiexp SourceBuilder)."""
+
+    def __init__(self, ctx, group, uncompressed: bytes, checked=True):
+        pb = 96 if group == BH_G1 else 192
+        assert len(uncompressed) % pb == 0
+        n = len(uncompressed) // pb
+        buf = np.frombuffer(uncompressed, dtype=np.uint8) if n else np.zeros(1, np.uint8)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_srs_upload(ctx.h, group, _ptr(buf), n, int(checked), ctypes.byref(h)), "bh_srs_upload")
+        self.h, self.group, self.ctx = h, group, ctx
+
+    def __len__(self):
+        return _lib.bh_srs_len(self.h)
+
+    def get(self, i):
+        out = np.zeros(96 if self.group == BH_G1 else 192, dtype=np.uint8)
+        _check(_lib.bh_srs_get(self.h, i, _ptr(out)))
+        return out.tobytes()
+
+    def __del__(self):
+        try:
+            _lib.bh_srs_free(self.h)
+        except Exception:
+            pass
+
+
+class FullDensity:
+    """multiexp.rs:96-115"""
+
+
+def multiexp(ctx, bases, offset, density, exponents, montgomery=False):
+    """multiexp::multiexp (multiexp.rs:252-281).  density: FullDensity/None or
+    a DensityTracker / list of bools; exponents: list of ints or an (n,4)
+    uint64 array (canonical, or Montgomery when montgomery=True).
+    Returns the uncompressed encoding of the affine result."""
+    if isinstance(exponents, np.ndarray):
+        ex = np.ascontiguousarray(exponents, dtype=np.uint64).reshape(-1, 4)
+    else:
+        ex = fr_to_mont(exponents) if montgomery else fr_to_canonical_limbs(exponents)
+    n = ex.shape[0]
+    bits = None
+    if density is not None and not isinstance(density, FullDensity) and density is not FullDensity:
+        bits = density.bv if hasattr(density, "bv") else list(density)
+    dw = density_words(bits) if bits is not None else None
+    out = np.zeros(96 if bases.group == BH_G1 else 192, dtype=np.uint8)
+    _check(_lib.bh_multiexp(ctx.h, bases.h, offset, _ptr(dw), len(bits) if bits is not None else 0,
+                            _ptr(ex) if n else None, n,
+                            BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, _ptr(out)),
+           "bh_multiexp")
+    return out.tobytes()
+
+
+# ------------------------------------------------------------------ EvaluationDomain
+class EvaluationDomain:
+    """domain.rs:21-190 over Scalar<Fr>; coefficients live as (m,4) Montgomery limbs."""
+
+    def __init__(self, ctx, coeffs):
+        """from_coeffs (domain.rs:47-79): coeffs = list of ints or (n,4) Montgomery array."""
+        arr = coeffs if isinstance(coeffs, np.ndarray) else fr_to_mont(coeffs)
+        arr = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 4)
+        m = ctypes.c_size_t()
+        e = ctypes.c_uint32()
+        _check(_lib.bh_domain_size(arr.shape[0], ctypes.byref(m), ctypes.byref(e)), "from_coeffs")
+        self.m, self.exp = m.value, e.value
+        self.coeffs = np.zeros((self.m, 4), dtype=np.uint64)
+        self.coeffs[: arr.shape[0]] = arr
+        self.ctx = ctx
+
+    from_coeffs = classmethod(lambda cls, ctx, coeffs: cls(ctx, coeffs))
+
+    def _run(self, f):
+        _check(f(self.ctx.h, _ptr(self.coeffs), self.exp))
+
+    def fft(self):
+        self._run(_lib.bh_fft)
+
+    def ifft(self):
+        self._run(_lib.bh_ifft)
+
+    def coset_fft(self):
+        self._run(_lib.bh_coset_fft)
+
+    def icoset_fft(self):
+        self._run(_lib.bh_icoset_fft)
+
+    def divide_by_z_on_coset(self):
+        self._run(_lib.bh_divide_by_z_on_coset)
+
+    def distribute_powers(self, g):
+        gm = fr_to_mont([g])[0]
+        _check(_lib.bh_distribute_powers(self.ctx.h, _ptr(self.coeffs), self.m, _ptr(gm)))
+
+    def mul_assign(self, other):
+        assert self.m == other.m
+        _check(_lib.bh_mul_assign(self.ctx.h, _ptr(self.coeffs), _ptr(other.coeffs), self.m))
+
+    def sub_assign(self, other):
+        assert self.m == other.m
+        _check(_lib.bh_sub_assign(self.ctx.h, _ptr(self.coeffs), _ptr(other.coeffs), self.m))
+
+    def into_coeffs(self):
+        return fr_from_mont(self.coeffs)
+
+
+def compute_h(ctx, a, b, c):
+    """H block of create_proof (prover.rs:210-231) -> list of m-1 ints."""
+    A, B, C = (x if isinstance(x, np.ndarray) else fr_to_mont(x) for x in (a, b, c))
+    n = A.shape[0]
+    m = ctypes.c_size_t()
+    _check(_lib.bh_domain_size(n, ctypes.byref(m), None))
+    out = np.zeros((max(m.value - 1, 1), 4), dtype=np.uint64)
+    hl = ctypes.c_size_t()
+    _check(_lib.bh_compute_h(ctx.h, _ptr(A), _ptr(B), _ptr(C), n, _ptr(out), ctypes.byref(hl)))
+    return fr_from_mont(out[: hl.value])
+
+
+# ------------------------------------------------------------------ Parameters
+class Parameters:
+    """Device-resident Parameters<Bls12> (groth16/mod.rs:224-247)."""
+
+    def __init__(self, ctx, handle):
+        self.ctx, self.h = ctx, handle
+
+    @classmethod
+    def read(cls, ctx, data: bytes, checked=True):
+        buf = np.frombuffer(data, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_params_load(ctx.h, _ptr(buf), len(data), int(checked), ctypes.byref(h)), "Parameters::read")
+        return cls(ctx, h)
+
+    @classmethod
+    def chain(cls, ctx, rounds, seed=7, alpha=6, beta=24, gamma=6, delta=24, tau=2):
+        h = ctypes.c_void_p()
+        _check(_lib.bh_chain_params(ctx.h, rounds, seed, alpha, beta, gamma, delta, tau, ctypes.byref(h)),
+               "bh_chain_params")
+        return cls(ctx, h)
+
+    def sizes(self):
+        out = (ctypes.c_size_t * 6)()
+        _check(_lib.bh_params_sizes(self.h, out))
+        return dict(zip(["h", "l", "a", "b_g1", "b_g2", "ic"], list(out)))
+
+    def write(self):
+        n = ctypes.c_size_t()
+        _check(_lib.bh_params_write(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint8)
+        _check(_lib.bh_params_write(self.h, _ptr(out), n.value, ctypes.byref(n)))
+        return out.tobytes()
+
+    def __del__(self):
+        try:
+            _lib.bh_params_free(self.h)
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------ R1CS host API (lib.rs)
+class Variable:
+    __slots__ = ("kind", "index")
+
+    def __init__(self, kind, index):
+        self.kind, self.index = kind, index
+
+
+ONE = Variable("input", 0)
+
+
+class LinearCombination:
+    """lib.rs:240-350"""
+
+    def __init__(self, terms=None):
+        self.terms = list(terms or [])
+
+    @staticmethod
+    def zero():
+        return LinearCombination()
+
+    def __add__(self, o):
+        if isinstance(o, Variable):
+            return LinearCombination(self.terms + [(o, 1)])
+        if isinstance(o, LinearCombination):
+            return LinearCombination(self.terms + o.terms)
+        coeff, x = o
+        if isinstance(x, LinearCombination):
+            return LinearCombination(self.terms + [(v, c * coeff) for v, c in x.terms])
+        return LinearCombination(self.terms + [(x, coeff)])
+
+    def __sub__(self, o):
+        if isinstance(o, Variable):
+            return LinearCombination(self.terms + [(o, -1)])
+        if isinstance(o, LinearCombination):
+            return LinearCombination(self.terms + [(v, -c) for v, c in o.terms])
+        coeff, x = o
+        if isinstance(x, LinearCombination):
+            return LinearCombination(self.terms + [(v, -c * coeff) for v, c in x.terms])
+        return LinearCombination(self.terms + [(x, -coeff)])
+
+
+class DensityTracker:
+    """multiexp.rs:117-157"""
+
+    def __init__(self):
+        self.bv = []
+
+    def add_element(self):
+        self.bv.append(False)
+
+    def inc(self, i):
+        self.bv[i] = True
+
+    def get_total_density(self):
+        return sum(self.bv)
+
+
+class ProvingAssignment:
+    """prover.rs:55-156 (host-side witness assignment and density tracking)."""
+
+    def __init__(self):
+        self.a_aux_density, self.b_input_density, self.b_aux_density = DensityTracker(), DensityTracker(), DensityTracker()
+        self.a, self.b, self.c = [], [], []
+        self.input_assignment, self.aux_assignment = [], []
+
+    @staticmethod
+    def one():
+        return ONE
+
+    def namespace(self, name):
+        return self
+
+    def alloc(self, name, f):
+        v = f()
+        if v is None:
+            raise AssignmentMissing()
+        self.aux_assignment.append(int(v) % R_MODULUS)
+        self.a_aux_density.add_element()
+        self.b_aux_density.add_element()
+        return Variable("aux", len(self.aux_assignment) - 1)
+
+    def alloc_input(self, name, f):
+        v = f()
+        if v is None:
+            raise AssignmentMissing()
+        self.input_assignment.append(int(v) % R_MODULUS)
+        self.b_input_density.add_element()
+        return Variable("input", len(self.input_assignment) - 1)
+
+    def _eval(self, lc, in_d, aux_d):
+        acc = 0
+        for v, coeff in lc.terms:
+            if v.kind == "input":
+                t = self.input_assignment[v.index]
+                if in_d is not None:
+                    in_d.inc(v.index)
+            else:
+                t = self.aux_assignment[v.index]
+                if aux_d is not None:
+                    aux_d.inc(v.index)
+            acc += t * coeff
+        return acc % R_MODULUS
+
+    def enforce(self, name, la, lb, lc):
+        z = LinearCombination.zero
+        self.a.append(self._eval(la(z()), None, self.a_aux_density))
+        self.b.append(self._eval(lb(z()), self.b_input_density, self.b_aux_density))
+        self.c.append(self._eval(lc(z()), None, None))
+
+
+def synthesize(circuit):
+    """prover.rs:187-204"""
+    p = ProvingAssignment()
+    p.alloc_input("", lambda: 1)
+    circuit.synthesize(p)
+    for i in range(len(p.input_assignment)):
+        p.enforce("", lambda lc, i=i: lc + Variable("input", i), lambda lc: lc, lambda lc: lc)
+    return p
+
+
+class Witness:
+    """A complete assignment resident in HBM (bh_witness)."""
+
+    def __init__(self, ctx, handle, num_constraints):
+        self.ctx, self.h, self.num_constraints = ctx, handle, num_constraints
+
+    @classmethod
+    def from_assignment(cls, ctx, p):
+        arrs = [fr_to_mont(x) for x in (p.a, p.b, p.c, p.input_assignment, p.aux_assignment)]
+        dens = [density_words(d.bv) for d in (p.a_aux_density, p.b_input_density, p.b_aux_density)]
+        h = ctypes.c_void_p()
+        _check(_lib.bh_witness_upload(ctx.h, _ptr(arrs[0]), _ptr(arrs[1]), _ptr(arrs[2]), len(p.a),
+                                      _ptr(arrs[3]), len(p.input_assignment), _ptr(arrs[4]),
+                                      len(p.aux_assignment), _ptr(dens[0]), _ptr(dens[1]), _ptr(dens[2]),
+                                      ctypes.byref(h)), "bh_witness_upload")
+        return cls(ctx, h, len(p.a))
+
+    @classmethod
+    def chain(cls, ctx, rounds, seed=7):
+        h = ctypes.c_void_p()
+        _check(_lib.bh_chain_witness(ctx.h, rounds, seed, ctypes.byref(h)), "bh_chain_witness")
+        return cls(ctx, h, 2 * rounds + 2)
+
+    def __del__(self):
+        try:
+            _lib.bh_witness_free(self.h)
+        except Exception:
+            pass
+
+
+def prove_witness(ctx, params, witness, r, s):
+    """create_proof after synthesis (prover.rs:206-349) -> Proof::write bytes (192)."""
+    out = np.zeros(192, dtype=np.uint8)
+    rr, ss = fr_to_canonical_limbs([r])[0], fr_to_canonical_limbs([s])[0]
+    _check(_lib.bh_prove_witness(ctx.h, params.h, witness.h, _ptr(rr), _ptr(ss), _ptr(out)), "create_proof")
+    return out.tobytes()
+
+
+def create_proof(ctx, circuit, params, r, s):
+    """prover.rs:175-350: synthesize on the host, prove on the device."""
+    p = synthesize(circuit)
+    w = Witness.from_assignment(ctx, p)
+    return prove_witness(ctx, params, w, r, s)
+
+
+def create_random_proof(ctx, circuit, params, rng=None):
+    """prover.rs:158-173: the fork ignores rng and uses r = 27134, s = 17146."""
+    return create_proof(ctx, circuit, params, 27134, 17146)

@@ -1,0 +1,755 @@
+// C ABI implementation: context, bases (SRS), multiexp, EvaluationDomain,
+// Parameters and the Groth16 prover core.  See include/bellman_hip.h for the
+// reference interface each entry point replaces.
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+
+#include "api_internal.h"
+
+using namespace bh;
+
+namespace bh {
+
+static thread_local hipError_t g_last_hip = hipSuccess;
+void set_last_hip_error(hipError_t e) { g_last_hip = e; }
+
+// ------------------------------------------------------------------ Fr host <-> device
+static const Fr& fr_two261() {
+  static Fr v = [] {
+    uint64_t two[4] = {2, 0, 0, 0};
+    uint64_t e[1] = {261};
+    return pow_vartime(from_int<4>(two), e, 1);
+  }();
+  return v;
+}
+static const Fr& fr_two261_inv() {
+  static Fr v = inv(fr_two261());
+  return v;
+}
+static inline void split29(const uint64_t raw[4], uint32_t out[9]) {
+  for (int i = 0; i < 9; i++) {
+    int bit = 29 * i, w = bit >> 6, sh = bit & 63;
+    uint64_t lo = raw[w] >> sh;
+    if (sh > 35 && w + 1 < 4) lo |= raw[w + 1] << (64 - sh);
+    out[i] = (uint32_t)(lo & 0x1fffffffu);
+  }
+}
+void fr_to_dev_limbs(const Fr& x, uint32_t out[9]) {
+  uint64_t raw[4];
+  to_int(mul(x, fr_two261()), raw);
+  split29(raw, out);
+}
+void fr_to_dev_packed(const Fr& x, uint32_t out[8]) {
+  uint64_t raw[4];
+  to_int(mul(x, fr_two261()), raw);
+  for (int i = 0; i < 4; i++) { out[2 * i] = (uint32_t)raw[i]; out[2 * i + 1] = (uint32_t)(raw[i] >> 32); }
+}
+Fr fr_from_dev_packed(const uint32_t in[8]) {
+  uint64_t raw[4];
+  for (int i = 0; i < 4; i++) raw[i] = (uint64_t)in[2 * i] | ((uint64_t)in[2 * i + 1] << 32);
+  // raw may be in [r, 2r): reduce
+  if (geq_p<4>(raw)) sub_p<4>(raw);
+  return mul(from_int<4>(raw), fr_two261_inv());
+}
+
+// ------------------------------------------------------------------ device point conversion
+// canonical packed coordinates -> device Montgomery packed; optional on-curve check
+template <bool G2>
+__global__ void __launch_bounds__(256) k_points_to_dev(uint32_t* pts, size_t n, int check, uint32_t* bad) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  constexpr int NC = G2 ? 4 : 2;  // DFp coordinates per point
+  DFp r2;
+#pragma unroll
+  for (int k = 0; k < 14; k++) r2.v[k] = FpCfg::R2[k];
+  DFp c[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) {
+    DFp x = fe_unpack<FpCfg>(pts + (i * NC + k) * 12);
+    c[k] = fe_reduce_full<FpCfg>(fe_mul<FpCfg>(x, r2));
+    fe_pack<FpCfg>(c[k], pts + (i * NC + k) * 12);
+  }
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < NC; k++)
+#pragma unroll
+    for (int l = 0; l < 14; l++) nz |= c[k].v[l];
+  if (check && nz) {  // (0,0) encodes the identity (never on the curve), skip it
+    DFp four = fe_add<FpCfg>(fe_add<FpCfg>(fe_one<FpCfg>(), fe_one<FpCfg>()),
+                            fe_add<FpCfg>(fe_one<FpCfg>(), fe_one<FpCfg>()));
+    bool ok;
+    if (!G2) {
+      DFp lhs = fe_sqr<FpCfg>(c[1]);
+      DFp rhs = fe_add<FpCfg>(fe_mul<FpCfg>(fe_sqr<FpCfg>(c[0]), c[0]), four);
+      ok = fe_is_zero<FpCfg>(fe_sub<FpCfg, 8>(lhs, rhs));
+    } else {
+      DFp2 x{c[0], c[1]}, y{c[2], c[3]};
+      DFp2 lhs = Fp2Ops::sqr(y);
+      DFp2 x3 = Fp2Ops::mul(Fp2Ops::sqr(x), x);
+      DFp2 rhs{fe_add<FpCfg>(x3.c0, four), fe_add<FpCfg>(x3.c1, four)};
+      DFp2 d = Fp2Ops::sub<16>(lhs, rhs);
+      ok = Fp2Ops::is_zero(d);
+    }
+    if (!ok) atomicOr(bad, 1u);
+  }
+}
+
+// ------------------------------------------------------------------ SRS
+// host affine points -> device (packed canonical words, then device conversion)
+bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_pts, size_t n, bh_srs* out) {
+  out->ctx = ctx;
+  out->group = group;
+  out->n = n;
+  out->identity_idx.clear();
+  const int words = group == BH_G1 ? 24 : 48;
+  std::vector<uint32_t> w((size_t)n * words);
+  for (size_t i = 0; i < n; i++) {
+    uint32_t* d = &w[i * words];
+    if (group == BH_G1) {
+      const AffinePt<Fp>& a = reinterpret_cast<const AffinePt<Fp>*>(host_pts)[i];
+      if (a.infinity) { out->identity_idx.push_back(i); memset(d, 0, words * 4); continue; }
+      uint64_t raw[6];
+      to_int(a.x, raw); memcpy(d, raw, 48);
+      to_int(a.y, raw); memcpy(d + 12, raw, 48);
+    } else {
+      const AffinePt<Fp2>& a = reinterpret_cast<const AffinePt<Fp2>*>(host_pts)[i];
+      if (a.infinity) { out->identity_idx.push_back(i); memset(d, 0, words * 4); continue; }
+      uint64_t raw[6];
+      to_int(a.x.c0, raw); memcpy(d, raw, 48);
+      to_int(a.x.c1, raw); memcpy(d + 12, raw, 48);
+      to_int(a.y.c0, raw); memcpy(d + 24, raw, 48);
+      to_int(a.y.c1, raw); memcpy(d + 36, raw, 48);
+    }
+  }
+  BH_TRY_HIP(out->pts.alloc(std::max<size_t>(n, 1) * words * 4));
+  if (n) {
+    BH_TRY_HIP(hipMemcpyAsync(out->pts.p, w.data(), n * words * 4, hipMemcpyHostToDevice, ctx->stream));
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (group == BH_G1)
+      hipLaunchKernelGGL(k_points_to_dev<false>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+                         0, (uint32_t*)nullptr);
+    else
+      hipLaunchKernelGGL(k_points_to_dev<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+                         0, (uint32_t*)nullptr);
+    BH_TRY_HIP(hipGetLastError());
+    BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return BH_OK;
+}
+
+// parse n uncompressed encodings; returns BH_ERR_INVALID_ENCODING / BH_ERR_NOT_ON_CURVE
+bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked,
+                                bool reject_identity, bh_srs* out) {
+  const size_t pb = group == BH_G1 ? 96 : 192;
+  const int words = group == BH_G1 ? 24 : 48;
+  out->ctx = ctx;
+  out->group = group;
+  out->n = n;
+  out->identity_idx.clear();
+  std::vector<uint32_t> w((size_t)n * words);
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* b = bytes + i * pb;
+    uint32_t* d = &w[i * words];
+    const uint8_t flags = b[0] >> 5;
+    if ((flags & 0x4) || (flags & 0x1)) return BH_ERR_INVALID_ENCODING;
+    if (flags & 0x2) {
+      for (size_t k = 0; k < pb; k++)
+        if ((k == 0 ? (b[0] & 0x1F) : b[k]) != 0) return BH_ERR_INVALID_ENCODING;
+      if (reject_identity) return BH_ERR_INVALID_ENCODING;
+      out->identity_idx.push_back(i);
+      memset(d, 0, words * 4);
+      continue;
+    }
+    // each 48-byte big-endian field element -> 12 LE words, canonical check
+    const int nf = group == BH_G1 ? 2 : 4;
+    for (int f = 0; f < nf; f++) {
+      // G2 wire order: x.c1, x.c0, y.c1, y.c0 ; device order: x.c0, x.c1, y.c0, y.c1
+      int dst = group == BH_G1 ? f : (f ^ 1);
+      const uint8_t* src = b + 48 * f;
+      uint64_t raw[6] = {0};
+      for (int k = 0; k < 48; k++) {
+        uint8_t byte = src[k];
+        if (f == 0 && k == 0) byte &= 0x1F;
+        raw[(47 - k) / 8] |= (uint64_t)byte << (8 * ((47 - k) % 8));
+      }
+      if (geq_p<6>(raw)) return BH_ERR_INVALID_ENCODING;
+      memcpy(d + 12 * dst, raw, 48);
+    }
+  }
+  BH_TRY_HIP(out->pts.alloc(std::max<size_t>(n, 1) * words * 4));
+  if (n) {
+    DevBuf bad;
+    BH_TRY_HIP(bad.alloc(4));
+    BH_TRY_HIP(hipMemsetAsync(bad.p, 0, 4, ctx->stream));
+    BH_TRY_HIP(hipMemcpyAsync(out->pts.p, w.data(), n * words * 4, hipMemcpyHostToDevice, ctx->stream));
+    unsigned blocks = (unsigned)((n + 255) / 256);
+    if (group == BH_G1)
+      hipLaunchKernelGGL(k_points_to_dev<false>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+                         checked, bad.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(k_points_to_dev<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+                         checked, bad.as<uint32_t>());
+    BH_TRY_HIP(hipGetLastError());
+    uint32_t hbad = 0;
+    BH_TRY_HIP(hipMemcpyAsync(&hbad, bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+    if (hbad) return BH_ERR_NOT_ON_CURVE;
+  }
+  return BH_OK;
+}
+
+// ------------------------------------------------------------------ MSM glue
+static inline Fp fp_from_dev_limbs(const uint32_t* limbs14) {
+  // unpacked 29-bit limbs (canonical) -> packed words -> host
+  uint32_t words[12] = {0};
+  for (int i = 0; i < 14; i++) {
+    const int bit = 29 * i;
+    const int wi = bit >> 5, sh = bit & 31;
+    uint64_t v = (uint64_t)limbs14[i] << sh;
+    words[wi] |= (uint32_t)v;
+    if (wi + 1 < 12) words[wi + 1] |= (uint32_t)(v >> 32);
+  }
+  return fp_from_dev_words(words);
+}
+
+Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, int W, int c) {
+  Jac<Fp> acc = jac_identity<Fp>();
+  for (int w = W - 1; w >= 0; w--) {
+    for (int k = 0; k < c; k++) acc = jac_dbl(acc);
+    const XYZZ<FpOps>& p = ws[w];
+    Jac<Fp> q = xyzz_to_jac(fp_from_dev_limbs(p.X.v), fp_from_dev_limbs(p.Y.v), fp_from_dev_limbs(p.ZZ.v),
+                            fp_from_dev_limbs(p.ZZZ.v));
+    acc = jac_add(acc, q);
+  }
+  return acc;
+}
+static inline bh::Fp2 fp2_from_dev(const DFp2& v) {
+  return bh::Fp2{fp_from_dev_limbs(v.c0.v), fp_from_dev_limbs(v.c1.v)};
+}
+Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, int W, int c) {
+  Jac<bh::Fp2> acc = jac_identity<bh::Fp2>();
+  for (int w = W - 1; w >= 0; w--) {
+    for (int k = 0; k < c; k++) acc = jac_dbl(acc);
+    const XYZZ<Fp2Ops>& p = ws[w];
+    Jac<bh::Fp2> q = xyzz_to_jac(fp2_from_dev(p.X), fp2_from_dev(p.Y), fp2_from_dev(p.ZZ), fp2_from_dev(p.ZZZ));
+    acc = jac_add(acc, q);
+  }
+  return acc;
+}
+
+static MsmTiming g_no_timing;
+
+bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
+                        const int32_t* d_idx, Jac<Fp>* out, float* acc_ms) {
+  if (n == 0) { *out = jac_identity<Fp>(); return BH_OK; }
+    MsmShape sh = msm_shape(n, ctx->window_override);
+  MsmTiming tm;
+  if (acc_ms) { tm.ev_acc_begin = ctx->ev[14]; tm.ev_acc_end = ctx->ev[15]; }
+  BH_TRY_HIP(msm_window_sums<G1Ops>(ctx->g1ws, ctx->stream, bases->pts.as<uint32_t>(), d_scalars, n, d_idx,
+                                    (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
+  *out = combine_g1(ctx->g1ws.host_window_sums, sh.W, sh.c);
+  return BH_OK;
+}
+bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
+                        const int32_t* d_idx, Jac<bh::Fp2>* out, float* acc_ms) {
+  if (n == 0) { *out = jac_identity<bh::Fp2>(); return BH_OK; }
+    MsmShape sh = msm_shape(n, ctx->window_override);
+  MsmTiming tm;
+  if (acc_ms) { tm.ev_acc_begin = ctx->ev[14]; tm.ev_acc_end = ctx->ev[15]; }
+  BH_TRY_HIP(msm_window_sums<G2Ops>(ctx->g2ws, ctx->stream, bases->pts.as<uint32_t>(), d_scalars, n, d_idx,
+                                    (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
+  *out = combine_g2(ctx->g2ws.host_window_sums, sh.W, sh.c);
+  return BH_OK;
+}
+
+// bellman's window rule (multiexp.rs:267-271) -- only used for error semantics
+static int bellman_window(size_t n) {
+  if (n < 32) return 3;
+  return (int)ceil(log((double)(uint32_t)n));
+}
+static inline uint64_t bits_window(const uint64_t* e, int skip, int c) {
+  uint64_t v = 0;
+  for (int i = 0; i < c; i++) {
+    int b = skip + i;
+    if (b < 256 && ((e[b >> 6] >> (b & 63)) & 1)) v |= 1ull << i;
+  }
+  return v;
+}
+
+// Exact reference error semantics (multiexp.rs:54-85 inside multiexp_inner's window
+// loop, then try_fold over the windows from the top, 244-249).
+bh_status multiexp_check(const bh_srs* bases, size_t base_offset, const uint64_t* density_words, size_t n,
+                         const uint64_t* exps, bool have_exps) {
+  size_t set = 0;
+  if (!density_words) set = n;
+  else {
+    for (size_t w = 0; w < n / 64; w++) set += (size_t)__builtin_popcountll(density_words[w]);
+    if (n % 64) set += (size_t)__builtin_popcountll(density_words[n / 64] & ((1ull << (n % 64)) - 1ull));
+  }
+  const size_t avail = base_offset < bases->n ? bases->n - base_offset : 0;
+  const bool eof = set > avail;
+  // identity bases actually reachable
+  bool any_identity = false;
+  for (size_t k : bases->identity_idx)
+    if (k >= base_offset && k - base_offset < set) any_identity = true;
+  if (!eof && !any_identity) return BH_OK;
+  if (!any_identity) return BH_ERR_UNEXPECTED_EOF;
+  if (!have_exps) return BH_ERR_UNEXPECTED_IDENTITY;
+  // walk entries, recording for each bellman window the first error position
+  const int c = bellman_window(n);
+  const int nw = (255 + c - 1) / c;  // skip in (0..255).step_by(c)
+  std::vector<size_t> first_err(nw, (size_t)-1);
+  std::vector<int> err_kind(nw, 0);
+  size_t cursor = base_offset, eof_pos = (size_t)-1;
+  size_t rank = 0;
+  std::vector<char> is_id(bases->n, 0);
+  for (size_t k : bases->identity_idx) is_id[k] = 1;
+  for (size_t i = 0; i < n; i++) {
+    bool d = density_words ? ((density_words[i >> 6] >> (i & 63)) & 1) : true;
+    if (!d) continue;
+    if (cursor >= bases->n) { eof_pos = i; break; }
+    if (is_id[cursor]) {
+      const uint64_t* e = exps + 4 * i;
+      bool zero = !(e[0] | e[1] | e[2] | e[3]);
+      bool one = e[0] == 1 && !(e[1] | e[2] | e[3]);
+      for (int w = 0; w < nw; w++) {
+        bool consumes;  // next() (not skip()) in window w
+        if (zero) consumes = false;
+        else if (one) consumes = (w == 0);
+        else consumes = bits_window(e, w * c, c) != 0;
+        if (consumes && first_err[w] == (size_t)-1) { first_err[w] = i; err_kind[w] = BH_ERR_UNEXPECTED_IDENTITY; }
+      }
+    }
+    cursor++;
+    rank++;
+  }
+  for (int w = nw - 1; w >= 0; w--) {
+    size_t p = first_err[w];
+    if (eof_pos != (size_t)-1 && (p == (size_t)-1 || eof_pos < p)) return BH_ERR_UNEXPECTED_EOF;
+    if (p != (size_t)-1) return err_kind[w];
+  }
+  return BH_OK;
+}
+
+// ------------------------------------------------------------------ domains
+static Fr fr_small(uint64_t v) { uint64_t x[4] = {v, 0, 0, 0}; return from_int<4>(x); }
+static Fr fr_pow_u64(const Fr& a, uint64_t e) { return pow_vartime(a, &e, 1); }
+
+static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, const Fr& hi_scale, int L,
+                                    int lo_bits) {
+  const size_t nlo = (size_t)1 << lo_bits;
+  const size_t nhi = (size_t)1 << (L > lo_bits ? L - lo_bits : 0);
+  std::vector<uint32_t> tl(nlo * 9), th(nhi * 9);
+  Fr x = Fr::one();
+  for (size_t j = 0; j < nlo; j++) { fr_to_dev_limbs(x, &tl[j * 9]); x = mul(x, g); }
+  const Fr step = x;  // g^(2^lo_bits)
+  Fr y = hi_scale;
+  for (size_t j = 0; j < nhi; j++) { fr_to_dev_limbs(y, &th[j * 9]); y = mul(y, step); }
+  BH_TRY_HIP(lo.alloc(tl.size() * 4));
+  BH_TRY_HIP(hi.alloc(th.size() * 4));
+  BH_TRY_HIP(hipMemcpyAsync(lo.p, tl.data(), tl.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  BH_TRY_HIP(hipMemcpyAsync(hi.p, th.data(), th.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return BH_OK;
+}
+
+bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
+  auto it = ctx->domains.find(L);
+  if (it != ctx->domains.end()) { *out = it->second.get(); return BH_OK; }
+  std::unique_ptr<Domain> d(new Domain());
+  d->L = L;
+  const size_t m = (size_t)1 << L;
+  // omega = root_of_unity^(2^(32-L))  (domain.rs:62-66)
+  uint64_t rou_raw[4] = {0x3829971f439f0d2bull, 0xb63683508c2280b9ull, 0xd09b681922c813b4ull, 0x16a2a19edfe81f20ull};
+  Fr omega = from_int<4>(rou_raw);
+  for (int i = L; i < 32; i++) omega = sqr(omega);
+  const Fr omegainv = inv(omega);
+  const Fr g = fr_small(7), ginv = inv(g);
+  d->minv = inv(fr_small(m));
+  d->zinv = inv(sub(fr_pow_u64(g, m), Fr::one()));  // domain.rs:129-151
+  // twiddles omega^j, j < m/2 (built on device from split tables)
+  const int tl = L >= 1 ? L - 1 : 0;
+  const int tb = (tl + 1) / 2;
+  DevBuf lo, hi;
+  for (int dir = 0; dir < 2; dir++) {
+    bh_status s = upload_split_table(ctx, lo, hi, dir == 0 ? omega : omegainv, Fr::one(), tl, tb);
+    if (s) return s;
+    DevBuf& tab = dir == 0 ? d->tw_fwd : d->tw_inv;
+    const size_t n = (size_t)1 << tl;
+    BH_TRY_HIP(tab.alloc(n * 9 * 4));
+    launch_expand_table(tab.as<uint32_t>(), n, lo.as<uint32_t>(), hi.as<uint32_t>(), tb, ctx->stream);
+    BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  d->lo_bits = (L + 1) / 2;
+  bh_status s;
+  if ((s = upload_split_table(ctx, d->coset_lo, d->coset_hi, g, d->minv, L, d->lo_bits))) return s;
+  if ((s = upload_split_table(ctx, d->icoset_lo, d->icoset_hi, ginv, d->minv, L, d->lo_bits))) return s;
+  if ((s = upload_split_table(ctx, d->gpow_lo, d->gpow_hi, g, Fr::one(), L, d->lo_bits))) return s;
+  uint32_t cst[3 * 9];
+  fr_to_dev_limbs(d->minv, cst);
+  fr_to_dev_limbs(d->zinv, cst + 9);
+  fr_to_dev_limbs(Fr::one(), cst + 18);
+  BH_TRY_HIP(d->consts.alloc(sizeof cst));
+  BH_TRY_HIP(hipMemcpy(d->consts.p, cst, sizeof cst, hipMemcpyHostToDevice));
+  *out = d.get();
+  ctx->domains[L] = std::move(d);
+  return BH_OK;
+}
+
+static FrConst conv_const(const uint32_t (&v)[9]) {
+  FrConst c;
+  memcpy(c.v, v, sizeof c.v);
+  return c;
+}
+
+// upload n Montgomery (bls12_381) Fr into dst (packed device form), zero-padding to `padded`
+bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst) {
+  if (padded > n) BH_TRY_HIP(hipMemsetAsync(dst + n * 8, 0, (padded - n) * 32, ctx->stream));
+  if (n) {
+    BH_TRY_HIP(hipMemcpyAsync(dst, host, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    launch_fr_convert(dst, dst, n, conv_const(FrConv::TO_DEV), 0, ctx->stream);
+  }
+  return BH_OK;
+}
+bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host) {
+  if (!n) return BH_OK;
+  launch_fr_convert(src, src, n, conv_const(FrConv::FROM_DEV), 1, ctx->stream);
+  BH_TRY_HIP(hipMemcpyAsync(host, src, n * 32, hipMemcpyDeviceToHost, ctx->stream));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  return BH_OK;
+}
+
+enum FftKind { FFT, IFFT, COSET_FFT, ICOSET_FFT };
+
+// natural -> natural transform of 2^L elements in d_a using d_tmp as scratch; result in d_a
+static bh_status run_fft(bh_ctx* ctx, Domain* D, FftKind kind, uint32_t* d_a, uint32_t* d_tmp) {
+  const int L = D->L;
+  const uint32_t* pre_lo = nullptr;
+  const uint32_t* pre_hi = nullptr;
+  if (kind == COSET_FFT) { pre_lo = D->gpow_lo.as<uint32_t>(); pre_hi = D->gpow_hi.as<uint32_t>(); }
+  launch_permute(d_a, d_tmp, L, pre_lo, pre_hi, D->lo_bits, ctx->stream);
+  const uint32_t* tw = (kind == FFT || kind == COSET_FFT) ? D->tw_fwd.as<uint32_t>() : D->tw_inv.as<uint32_t>();
+  const uint32_t* post_lo = nullptr;
+  const uint32_t* post_hi = nullptr;
+  int post_bits = D->lo_bits;
+  if (kind == IFFT) { post_hi = D->consts.as<uint32_t>(); post_bits = -1; }
+  if (kind == ICOSET_FFT) { post_lo = D->icoset_lo.as<uint32_t>(); post_hi = D->icoset_hi.as<uint32_t>(); }
+  launch_ntt(d_tmp, L, false, tw, post_lo, post_hi, post_bits, ctx->stream);
+  BH_TRY_HIP(hipMemcpyAsync(d_a, d_tmp, ((size_t)32) << L, hipMemcpyDeviceToDevice, ctx->stream));
+  BH_TRY_HIP(hipGetLastError());
+  return BH_OK;
+}
+
+static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind kind) {
+  if (!ctx || !coeffs || log_m >= 32) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  Domain* D;
+  bh_status s = ctx_domain(ctx, (int)log_m, &D);
+  if (s) return s;
+  const size_t m = (size_t)1 << log_m;
+  BH_TRY_HIP(ctx->staging.alloc(m * 32));
+  BH_TRY_HIP(ctx->staging2.alloc(m * 32));
+  if ((s = upload_fr(ctx, coeffs, m, m, ctx->staging.as<uint32_t>()))) return s;
+  if ((s = run_fft(ctx, D, kind, ctx->staging.as<uint32_t>(), ctx->staging2.as<uint32_t>()))) return s;
+  return download_fr(ctx, ctx->staging.as<uint32_t>(), m, coeffs);
+}
+
+// H pipeline on device-resident a|b|c (3*m packed device form, natural order). On return
+// d_abc's first m entries hold h coefficients in BIT-REVERSED order (device form).
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc) {
+  const int L = D->L;
+  const size_t m = (size_t)1 << L;
+  uint32_t* a = d_abc;
+  uint32_t* b = d_abc + m * 8;
+  uint32_t* c = d_abc + 2 * m * 8;
+  // prover.rs:214-219: ifft (DIF, omega^-1) with m^-1 * g^i fused = ifft + distribute_powers(g);
+  // then fft (DIT, bit-reversed -> natural) = coset_fft
+  for (uint32_t* x : {a, b, c}) {
+    launch_ntt(x, L, true, D->tw_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
+               D->lo_bits, ctx->stream);
+    launch_ntt(x, L, false, D->tw_fwd.as<uint32_t>(), nullptr, nullptr, 0, ctx->stream);
+  }
+  // prover.rs:221-225: a*b - c, divide_by_z_on_coset
+  launch_pointwise(a, b, c, m, 2, D->consts.as<uint32_t>() + 9, ctx->stream);
+  // prover.rs:226: icoset_fft = ifft + distribute_powers(g^-1), fused as above (output bit-reversed)
+  launch_ntt(a, L, true, D->tw_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
+             D->lo_bits, ctx->stream);
+  BH_TRY_HIP(hipGetLastError());
+  return BH_OK;
+}
+
+}  // namespace bh
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* bh_status_string(bh_status s) {
+  switch (s) {
+    case BH_OK: return "ok";
+    case BH_ERR_UNEXPECTED_IDENTITY: return "encountered an identity element in the CRS";
+    case BH_ERR_UNEXPECTED_EOF: return "I/O error: expected more bases from source";
+    case BH_ERR_POLY_DEGREE_TOO_LARGE: return "polynomial degree is too large";
+    case BH_ERR_DENSITY_SIZE_MISMATCH: return "density query size differs from the number of exponents";
+    case BH_ERR_UNCONSTRAINED_VARIABLE: return "auxiliary variable was unconstrained";
+    case BH_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case BH_ERR_INVALID_ENCODING: return "invalid point encoding";
+    case BH_ERR_NOT_ON_CURVE: return "point not on curve";
+    case BH_ERR_OUT_OF_MEMORY: return "device out of memory";
+    case BH_ERR_HIP: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}
+
+int bh_version(void) { return 1; }
+
+bh_status bh_ctx_create(int device, bh_ctx** out) {
+  if (!out) return BH_ERR_INVALID_ARGUMENT;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return BH_ERR_HIP;
+  BH_TRY_HIP(hipSetDevice(device));
+  bh_ctx* c = new bh_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  *out = c;
+  return BH_OK;
+}
+
+bh_status bh_ctx_destroy(bh_ctx* ctx) {
+  if (!ctx) return BH_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->g1ws.release();
+  ctx->g2ws.release();
+  ctx->domains.clear();
+  for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return BH_OK;
+}
+
+bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domain) {
+  if (!ctx) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  if (max_msm_len) {
+    BH_TRY_HIP(ctx->g1ws.reserve(max_msm_len));
+    BH_TRY_HIP(ctx->g2ws.reserve(max_msm_len));
+  }
+  size_t n = std::max(max_msm_len, (size_t)1 << max_log_domain);
+  BH_TRY_HIP(ctx->staging.alloc(n * 32));
+  BH_TRY_HIP(ctx->staging2.alloc(n * 32));
+  BH_TRY_HIP(ctx->idx.alloc(n * 4));
+  BH_TRY_HIP(ctx->dtmp.alloc((n / 64 + 2) * 4));
+  BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(n / 64 + 2) * 4 + 64));
+  BH_TRY_HIP(ctx->hbuf.alloc(((size_t)1 << max_log_domain) * 32));
+  if (max_log_domain) {
+    Domain* D;
+    bh_status s = ctx_domain(ctx, (int)max_log_domain, &D);
+    if (s) return s;
+  }
+  return BH_OK;
+}
+
+bh_status bh_ctx_set_window(bh_ctx* ctx, int c) {
+  if (!ctx || c < 0 || c > 20 || c == 1) return BH_ERR_INVALID_ARGUMENT;
+  ctx->window_override = c;
+  return BH_OK;
+}
+
+// ---------------------------------------------------------------- SRS
+bh_status bh_srs_upload(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bh_srs** out) {
+  if (!ctx || !out || (group != BH_G1 && group != BH_G2) || (n && !bytes)) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  bh_srs* s = new bh_srs();
+  bh_status st = srs_from_bytes(ctx, group, bytes, n, checked, false, s);
+  if (st) { delete s; return st; }
+  *out = s;
+  return BH_OK;
+}
+
+bh_status bh_srs_free(bh_srs* srs) {
+  delete srs;
+  return BH_OK;
+}
+size_t bh_srs_len(const bh_srs* srs) { return srs ? srs->n : 0; }
+
+bh_status bh_srs_get(const bh_srs* srs, size_t i, uint8_t* out) {
+  if (!srs || !out || i >= srs->n) return BH_ERR_INVALID_ARGUMENT;
+  const int words = srs->group == BH_G1 ? 24 : 48;
+  uint32_t w[48];
+  BH_TRY_HIP(hipMemcpy(w, srs->pts.as<uint32_t>() + i * words, words * 4, hipMemcpyDeviceToHost));
+  bool inf = std::find(srs->identity_idx.begin(), srs->identity_idx.end(), i) != srs->identity_idx.end();
+  if (srs->group == BH_G1) {
+    AffinePt<Fp> a{fp_from_dev_words(w), fp_from_dev_words(w + 12), inf};
+    g1_to_uncompressed(a, out);
+  } else {
+    AffinePt<bh::Fp2> a{bh::Fp2{fp_from_dev_words(w), fp_from_dev_words(w + 12)},
+                        bh::Fp2{fp_from_dev_words(w + 24), fp_from_dev_words(w + 36)}, inf};
+    g2_to_uncompressed(a, out);
+  }
+  return BH_OK;
+}
+
+// ---------------------------------------------------------------- multiexp
+bh_status bh_multiexp(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint64_t* density_words,
+                      size_t density_len, const uint64_t* exponents, size_t n, int scalar_format, uint8_t* out) {
+  if (!ctx || !bases || !out || (n && !exponents)) return BH_ERR_INVALID_ARGUMENT;
+  if (scalar_format != BH_SCALARS_CANONICAL && scalar_format != BH_SCALARS_MONTGOMERY) return BH_ERR_INVALID_ARGUMENT;
+  if (density_words && density_len != n) return BH_ERR_DENSITY_SIZE_MISMATCH;
+  if (n > 0x7fffffffull) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  // error semantics first (needs canonical exponents only when identity bases are reachable)
+  std::vector<uint64_t> canon;
+  const uint64_t* ex_c = exponents;
+  if (scalar_format == BH_SCALARS_MONTGOMERY && !bases->identity_idx.empty()) {
+    canon.resize(n * 4);
+    for (size_t i = 0; i < n; i++) {
+      Fr x;
+      memcpy(x.v, exponents + 4 * i, 32);
+      fr_to_canonical(x, &canon[4 * i]);
+    }
+    ex_c = canon.data();
+  }
+  bh_status st = multiexp_check(bases, base_offset, density_words, n, ex_c, true);
+  if (st) return st;
+  BH_TRY_HIP(ctx->staging.alloc(std::max<size_t>(n, 1) * 32));
+  BH_TRY_HIP(ctx->staging2.alloc(std::max<size_t>(n, 1) * 32));
+  uint32_t* d_sc = ctx->staging2.as<uint32_t>();
+  if (n) {
+    BH_TRY_HIP(hipMemcpyAsync(ctx->staging.p, exponents, n * 32, hipMemcpyHostToDevice, ctx->stream));
+    BH_TRY_HIP(scalars_prepare(ctx->staging.as<uint32_t>(), d_sc, n, scalar_format == BH_SCALARS_MONTGOMERY ? 1 : 0,
+                               0, ctx->stream));
+  }
+  const int32_t* d_idx = nullptr;
+  DevBuf dwords;
+  if (density_words && n) {
+    const size_t nw = (n + 63) / 64;
+    BH_TRY_HIP(dwords.alloc(nw * 8));
+    BH_TRY_HIP(ctx->idx.alloc(n * 4));
+    BH_TRY_HIP(ctx->dtmp.alloc((nw + 1) * 4));
+    BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(nw + 1) * 4 + 64));
+    BH_TRY_HIP(hipMemcpyAsync(dwords.p, density_words, nw * 8, hipMemcpyHostToDevice, ctx->stream));
+    BH_TRY_HIP(density_index(dwords.as<uint64_t>(), n, (uint32_t)base_offset, ctx->idx.as<int32_t>(),
+                             ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), ctx->stream));
+    d_idx = ctx->idx.as<int32_t>();
+  }
+  if (bases->group == BH_G1) {
+    Jac<Fp> r;
+    if ((st = msm_g1_device(ctx, bases, base_offset, d_sc, n, d_idx, &r, nullptr))) return st;
+    g1_to_uncompressed(jac_to_affine(r), out);
+  } else {
+    Jac<bh::Fp2> r;
+    if ((st = msm_g2_device(ctx, bases, base_offset, d_sc, n, d_idx, &r, nullptr))) return st;
+    g2_to_uncompressed(jac_to_affine(r), out);
+  }
+  return BH_OK;
+}
+
+// ---------------------------------------------------------------- EvaluationDomain
+bh_status bh_domain_size(size_t len, size_t* m, uint32_t* log_m) {
+  size_t mm = 1;
+  uint32_t e = 0;
+  while (mm < len) {
+    mm *= 2;
+    e++;
+    if (e >= 32) return BH_ERR_POLY_DEGREE_TOO_LARGE;  // domain.rs:51-60 (S = 32)
+  }
+  if (m) *m = mm;
+  if (log_m) *log_m = e;
+  return BH_OK;
+}
+
+bh_status bh_fft(bh_ctx* ctx, uint64_t* a, uint32_t log_m) { return host_fft(ctx, a, log_m, FFT); }
+bh_status bh_ifft(bh_ctx* ctx, uint64_t* a, uint32_t log_m) { return host_fft(ctx, a, log_m, IFFT); }
+bh_status bh_coset_fft(bh_ctx* ctx, uint64_t* a, uint32_t log_m) { return host_fft(ctx, a, log_m, COSET_FFT); }
+bh_status bh_icoset_fft(bh_ctx* ctx, uint64_t* a, uint32_t log_m) { return host_fft(ctx, a, log_m, ICOSET_FFT); }
+
+bh_status bh_distribute_powers(bh_ctx* ctx, uint64_t* coeffs, size_t len, const uint64_t g_mont[4]) {
+  if (!ctx || (len && !coeffs) || !g_mont) return BH_ERR_INVALID_ARGUMENT;
+  if (!len) return BH_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  int L = 0;
+  while (((size_t)1 << L) < len) L++;
+  Fr g;
+  memcpy(g.v, g_mont, 32);
+  DevBuf lo, hi;
+  const int lo_bits = (L + 1) / 2;
+  bh_status s = upload_split_table(ctx, lo, hi, g, Fr::one(), L, lo_bits);
+  if (s) return s;
+  BH_TRY_HIP(ctx->staging.alloc(len * 32));
+  if ((s = upload_fr(ctx, coeffs, len, len, ctx->staging.as<uint32_t>()))) return s;
+  launch_scale(ctx->staging.as<uint32_t>(), len, lo.as<uint32_t>(), hi.as<uint32_t>(), lo_bits, nullptr, ctx->stream);
+  return download_fr(ctx, ctx->staging.as<uint32_t>(), len, coeffs);
+}
+
+bh_status bh_divide_by_z_on_coset(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m) {
+  if (!ctx || !coeffs || log_m >= 32) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  Domain* D;
+  bh_status s = ctx_domain(ctx, (int)log_m, &D);
+  if (s) return s;
+  const size_t m = (size_t)1 << log_m;
+  BH_TRY_HIP(ctx->staging.alloc(m * 32));
+  if ((s = upload_fr(ctx, coeffs, m, m, ctx->staging.as<uint32_t>()))) return s;
+  launch_scale(ctx->staging.as<uint32_t>(), m, nullptr, nullptr, 0, D->consts.as<uint32_t>() + 9, ctx->stream);
+  return download_fr(ctx, ctx->staging.as<uint32_t>(), m, coeffs);
+}
+
+static bh_status host_pointwise(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len, int op) {
+  if (!ctx || (len && (!a || !b))) return BH_ERR_INVALID_ARGUMENT;
+  if (!len) return BH_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  BH_TRY_HIP(ctx->staging.alloc(len * 32));
+  BH_TRY_HIP(ctx->staging2.alloc(len * 32));
+  bh_status s;
+  if ((s = upload_fr(ctx, a, len, len, ctx->staging.as<uint32_t>()))) return s;
+  if ((s = upload_fr(ctx, b, len, len, ctx->staging2.as<uint32_t>()))) return s;
+  launch_pointwise(ctx->staging.as<uint32_t>(), ctx->staging2.as<uint32_t>(), nullptr, len, op, nullptr, ctx->stream);
+  return download_fr(ctx, ctx->staging.as<uint32_t>(), len, a);
+}
+bh_status bh_mul_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len) {
+  return host_pointwise(ctx, a, b, len, 0);
+}
+bh_status bh_sub_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len) {
+  return host_pointwise(ctx, a, b, len, 1);
+}
+
+bh_status bh_compute_h(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c, size_t nc,
+                       uint64_t* h_out, size_t* h_len) {
+  if (!ctx || (nc && (!a || !b || !c)) || !h_out) return BH_ERR_INVALID_ARGUMENT;
+  size_t m;
+  uint32_t L;
+  bh_status s = bh_domain_size(nc, &m, &L);
+  if (s) return s;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  Domain* D;
+  if ((s = ctx_domain(ctx, (int)L, &D))) return s;
+  BH_TRY_HIP(ctx->staging.alloc(3 * m * 32));
+  BH_TRY_HIP(ctx->staging2.alloc(m * 32));
+  uint32_t* abc = ctx->staging.as<uint32_t>();
+  if ((s = upload_fr(ctx, a, nc, m, abc))) return s;
+  if ((s = upload_fr(ctx, b, nc, m, abc + m * 8))) return s;
+  if ((s = upload_fr(ctx, c, nc, m, abc + 2 * m * 8))) return s;
+  if ((s = run_h_pipeline(ctx, D, abc))) return s;
+  // bit-reversed -> natural
+  launch_permute(abc, ctx->staging2.as<uint32_t>(), (int)L, nullptr, nullptr, 0, ctx->stream);
+  if ((s = download_fr(ctx, ctx->staging2.as<uint32_t>(), m - 1, h_out))) return s;
+  if (h_len) *h_len = m - 1;
+  return BH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+// Internal types shared by the C ABI implementation files.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/bellman_hip.h"
+#include "host_arith.h"
+#include "msm.h"
+#include "ntt.h"
+
+namespace bh {
+
+#define BH_TRY_HIP(expr)                                  \
+  do {                                                    \
+    hipError_t _e = (expr);                               \
+    if (_e != hipSuccess) {                               \
+      bh::set_last_hip_error(_e);                         \
+      return (_e == hipErrorOutOfMemory) ? BH_ERR_OUT_OF_MEMORY : BH_ERR_HIP; \
+    }                                                     \
+  } while (0)
+
+void set_last_hip_error(hipError_t e);
+
+// device buffer owning wrapper
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t b) {
+    if (b <= bytes && p) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+    hipError_t e = hipMalloc(&p, b ? b : 16);
+    if (e == hipSuccess) bytes = b;
+    return e;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// NTT domain tables for one log size (device, unpacked 9-limb entries)
+struct Domain {
+  int L = -1;
+  DevBuf tw_fwd, tw_inv;                  // omega^j, omega^-j, j < m/2
+  DevBuf coset_lo, coset_hi;              // g^i split tables, hi folded with m^-1   (ifft -> coset)
+  DevBuf icoset_lo, icoset_hi;            // g^-i split, hi folded with m^-1        (icoset)
+  DevBuf gpow_lo, gpow_hi;                // g^i (no m^-1)                           (coset_fft input)
+  DevBuf consts;                          // [0] m^-1, [1] 1/Z(g), [2] one
+  int lo_bits = 0;
+  Fr minv, zinv;
+};
+
+struct bh_ctx_impl;
+}  // namespace bh
+
+struct bh_srs {
+  bh_ctx* ctx = nullptr;
+  int group = BH_G1;
+  size_t n = 0;
+  bh::DevBuf pts;                    // packed affine, device Montgomery
+  std::vector<size_t> identity_idx;  // indices of points at infinity (rejected by next())
+};
+
+struct bh_params {
+  bh_ctx* ctx = nullptr;
+  // VerifyingKey (host form)
+  bh::AffinePt<bh::Fp> alpha_g1, beta_g1, delta_g1;
+  bh::AffinePt<bh::Fp2> beta_g2, gamma_g2, delta_g2;
+  std::vector<bh::AffinePt<bh::Fp>> ic;
+  bh_srs h, l, a, b_g1, b_g2;
+};
+
+struct bh_witness {
+  bh_ctx* ctx = nullptr;
+  size_t num_constraints = 0, m = 0, num_inputs = 0, num_aux = 0;
+  int log_m = 0;
+  bh::DevBuf abc;          // 3 * m packed device-Montgomery Fr (a | b | c), zero padded
+  bh::DevBuf inputs, aux;  // canonical packed scalars
+  bh::DevBuf dens;         // a_aux | b_input | b_aux density words
+  size_t a_aux_words = 0, b_in_words = 0, b_aux_words = 0;
+  std::vector<uint64_t> a_aux_density, b_input_density, b_aux_density;  // host copies (EOF checks)
+  size_t a_aux_total = 0, b_in_total = 0, b_aux_total = 0;
+};
+
+struct bh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int window_override = 0;
+  bh::MsmWorkspace<G1Ops> g1ws;
+  bh::MsmWorkspace<G2Ops> g2ws;
+  std::map<int, std::unique_ptr<bh::Domain>> domains;
+  bh::DevBuf staging;     // generic host->device staging (scalars, polynomials)
+  bh::DevBuf staging2;
+  bh::DevBuf idx;         // density index map
+  bh::DevBuf dtmp;        // density scan tmp
+  bh::DevBuf dscan;       // scan scratch
+  bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
+  hipEvent_t ev[16] = {};
+  double last_timings[8] = {};
+  std::mutex mu;
+};
+
+namespace bh {
+bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out);
+// host <-> device Fr helpers
+void fr_to_dev_limbs(const Fr& x, uint32_t out[9]);
+void fr_to_dev_packed(const Fr& x, uint32_t out[8]);
+Fr fr_from_dev_packed(const uint32_t in[8]);
+// combine per-window sums (host Horner, multiexp.rs:244-249)
+Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, int W, int c);
+Jac<Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, int W, int c);
+// run one MSM whose scalars/index map are already on the device; returns result on host
+bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
+                        const int32_t* d_idx, Jac<Fp>* out, float* acc_ms);
+bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
+                        const int32_t* d_idx, Jac<Fp2>* out, float* acc_ms);
+bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst);
+bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc);
+bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,
+                         bh_srs* out);
+// reference-exact error semantics of multiexp (EOF / identity), host side
+bh_status multiexp_check(const bh_srs* bases, size_t base_offset, const uint64_t* density_words, size_t n,
+                         const uint64_t* exps_canonical, bool need_exps);
+bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_affine_g1_or_g2, size_t n, bh_srs* out);
+}  // namespace bh

@@ -1,0 +1,15 @@
+// Host interface of the device fixed-base scalar multiplication (crs.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "curve.cuh"
+
+namespace bh {
+// d_table: 32*255 packed affine points T[w][d-1] = d*2^(8w)*G (device Montgomery, canonical)
+// d_scalars: n canonical scalars (8 LE u32 words); non-zero scalars only (results are never infinity)
+// d_xyzz: n*sizeof(XYZZ) scratch; d_scratch: n*sizeof(field) scratch; d_out: n packed affine points
+template <class C>
+hipError_t fixed_base_batch(const uint32_t* d_table, const uint32_t* d_scalars, size_t n, void* d_xyzz,
+                            void* d_scratch, uint32_t* d_out, hipStream_t st);
+}  // namespace bh

@@ -1,0 +1,155 @@
+// Device group law for BLS12-381 G1 (over Fp) and G2 (over Fp2), a = 0.
+//
+// Bucket accumulators use extended Jacobian "XYZZ" coordinates
+// (x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2): a mixed addition with an affine base
+// costs 8M + 2S and needs no inversion (EFD madd-2008-s / add-2008-s /
+// dbl-2008-s / mdbl-2008-s).  Exceptional cases (P == Q, P == -Q, identity)
+// are handled exactly, so results are canonical group elements and compare
+// bit-exactly with bls12_381's projective arithmetic after normalisation.
+//
+// Bounds (multiples of p, see field.cuh): with MB = product bound of the field,
+//   X < XB = MB + K1,  Y < YB = MB + K3,  ZZ, ZZZ < MB
+// and every subtraction constant K is chosen >= the subtrahend's bound.
+#pragma once
+#include "field.cuh"
+
+constexpr uint32_t bh_pow2_ceil(uint32_t x) {
+  uint32_t r = 1;
+  while (r < x) r <<= 1;
+  return r;
+}
+
+template <class F>
+struct XYZZ {
+  typename F::T X, Y, ZZ, ZZZ;
+};
+
+template <class F>
+struct Affine {
+  typename F::T x, y;
+};
+
+template <class F>
+struct CurveOps {
+  using T = typename F::T;
+  using P = XYZZ<F>;
+  using A = Affine<F>;
+  static constexpr uint32_t MB = F::MB;
+  static constexpr uint32_t K1 = bh_pow2_ceil(3 * MB);
+  static constexpr uint32_t XB = MB + K1;
+  static constexpr uint32_t K2 = bh_pow2_ceil(XB);
+  static constexpr uint32_t K3 = bh_pow2_ceil(MB);
+  static constexpr uint32_t YB = MB + K3;
+  static constexpr uint32_t KX = K2;
+  static constexpr uint32_t KY = bh_pow2_ceil(YB);
+  static_assert(MB + KX < 128 && MB + KY < 128, "is_zero bound");
+
+  static BH_DEV P identity() {
+    P r;
+    r.X = F::zero(); r.Y = F::zero(); r.ZZ = F::zero(); r.ZZZ = F::zero();
+    return r;
+  }
+  static BH_DEV bool is_identity(const P& p) { return F::is_zero(p.ZZ); }
+
+  static BH_DEV P from_affine(const A& a) {
+    P r;
+    r.X = a.x; r.Y = a.y; r.ZZ = F::one(); r.ZZZ = F::one();
+    return r;
+  }
+
+  // 2*(x, y) for an affine point (mdbl-2008-s)
+  static BH_DEV P dbl_affine(const A& a) {
+    T U = F::add(a.y, a.y);
+    T V = F::sqr(U);
+    T W = F::mul(U, V);
+    T S = F::mul(a.x, V);
+    T xx = F::sqr(a.x);
+    T M = F::add(F::add(xx, xx), xx);
+    P r;
+    r.X = F::template sub<K1>(F::sqr(M), F::add(S, S));
+    r.Y = F::template sub<K3>(F::mul(M, F::template sub<K2>(S, r.X)), F::mul(W, a.y));
+    r.ZZ = V;
+    r.ZZZ = W;
+    return r;
+  }
+
+  // 2*p (dbl-2008-s); identity stays identity (ZZ' = V*ZZ ≡ 0)
+  static BH_DEV P dbl(const P& p) {
+    T U = F::add(p.Y, p.Y);
+    T V = F::sqr(U);
+    T W = F::mul(U, V);
+    T S = F::mul(p.X, V);
+    T xx = F::sqr(p.X);
+    T M = F::add(F::add(xx, xx), xx);
+    P r;
+    r.X = F::template sub<K1>(F::sqr(M), F::add(S, S));
+    r.Y = F::template sub<K3>(F::mul(M, F::template sub<K2>(S, r.X)), F::mul(W, p.Y));
+    r.ZZ = F::mul(V, p.ZZ);
+    r.ZZZ = F::mul(W, p.ZZZ);
+    return r;
+  }
+
+  // p + a, a affine and not the identity (madd-2008-s)
+  static BH_DEV P madd(const P& p, const A& a) {
+    if (is_identity(p)) return from_affine(a);
+    T U2 = F::mul(a.x, p.ZZ);
+    T S2 = F::mul(a.y, p.ZZZ);
+    T Pd = F::template sub<KX>(U2, p.X);
+    T R = F::template sub<KY>(S2, p.Y);
+    if (F::is_zero(Pd)) {
+      if (F::is_zero(R)) return dbl_affine(a);
+      return identity();
+    }
+    T PP = F::sqr(Pd);
+    T PPP = F::mul(Pd, PP);
+    T Q = F::mul(p.X, PP);
+    P r;
+    r.X = F::template sub<K1>(F::sqr(R), F::add(PPP, F::add(Q, Q)));
+    r.Y = F::template sub<K3>(F::mul(R, F::template sub<K2>(Q, r.X)), F::mul(p.Y, PPP));
+    r.ZZ = F::mul(p.ZZ, PP);
+    r.ZZZ = F::mul(p.ZZZ, PPP);
+    return r;
+  }
+
+  // p + q (add-2008-s)
+  static BH_DEV P add(const P& p, const P& q) {
+    if (is_identity(p)) return q;
+    if (is_identity(q)) return p;
+    T U1 = F::mul(p.X, q.ZZ);
+    T U2 = F::mul(q.X, p.ZZ);
+    T S1 = F::mul(p.Y, q.ZZZ);
+    T S2 = F::mul(q.Y, p.ZZZ);
+    T Pd = F::template sub<K3>(U2, U1);
+    T R = F::template sub<K3>(S2, S1);
+    if (F::is_zero(Pd)) {
+      if (F::is_zero(R)) return dbl(p);
+      return identity();
+    }
+    T PP = F::sqr(Pd);
+    T PPP = F::mul(Pd, PP);
+    T Q = F::mul(U1, PP);
+    P r;
+    r.X = F::template sub<K1>(F::sqr(R), F::add(PPP, F::add(Q, Q)));
+    r.Y = F::template sub<K3>(F::mul(R, F::template sub<K2>(Q, r.X)), F::mul(S1, PPP));
+    r.ZZ = F::mul(F::mul(p.ZZ, q.ZZ), PP);
+    r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
+    return r;
+  }
+
+  static BH_DEV A neg_affine(const A& a) {
+    A r;
+    r.x = a.x;
+    r.y = F::neg_canonical(a.y);
+    return r;
+  }
+
+  // canonical coordinates (each in [0,p)) for hand-off to the host
+  static BH_DEV P reduce(const P& p) {
+    P r;
+    r.X = F::reduce(p.X); r.Y = F::reduce(p.Y); r.ZZ = F::reduce(p.ZZ); r.ZZZ = F::reduce(p.ZZZ);
+    return r;
+  }
+};
+
+using G1Ops = CurveOps<FpOps>;
+using G2Ops = CurveOps<Fp2Ops>;

@@ -1,0 +1,333 @@
+// Device finite-field arithmetic for BLS12-381 on gfx950.
+//
+// Representation: N little-endian limbs of 29 bits held in uint32 (DFp: N=14,
+// Montgomery R = 2^406; Fr: N=9, R = 2^261).  Products of two limbs are < 2^58,
+// so a 64-bit column accumulator absorbs all 2N products of one column of the
+// product-scanning (FIPS) Montgomery multiplication with no carry handling:
+// every product is a single v_mad_u64_u32 (microbenchmarked on MI355X at
+// 77 G DFp-mul/s vs 46 G for 32-bit-limb CIOS, tools/microbench/fpbench.hip).
+//
+// Lazy reduction: because R/p >= 2^25 (DFp) and R/q >= 2^6 (Fr), montgomery
+// multiplication of inputs a < A*p, b < B*p returns a value < 2p whenever
+// A*B < 2^25 (DFp) / 2^6 (Fr).  Additions therefore never reduce; subtraction
+// adds a constant multiple K*p.  Values are brought to [0,p) only when they
+// leave the device (`reduce_full`) and equality tests use `is_zero` (x ≡ 0 mod
+// p for x < 128p) which costs one 32-bit multiply in the common (non-zero) case.
+//
+// The arithmetic restates the field ops bls12_381 0.6.0 performs for the
+// reference hot path (multiexp.rs:39,217,231-232,248; domain.rs:250-257).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "constants.h"
+
+#define BH_LIMB_BITS 29
+#define BH_LIMB_MASK 0x1fffffffu
+#define BH_DEV __device__ __forceinline__
+
+template <class C>
+struct Fe {
+  uint32_t v[C::N];
+};
+
+// ---------------------------------------------------------------- constexpr K*p limbs
+template <class C, uint32_t K>
+struct KP {
+  struct L { uint32_t v[C::N]; };
+  static constexpr L make() {
+    L l{};
+    uint64_t carry = 0;
+    for (int i = 0; i < C::N; i++) {
+      uint64_t t = (uint64_t)C::P[i] * K + carry;
+      l.v[i] = (uint32_t)(t & BH_LIMB_MASK);
+      carry = t >> BH_LIMB_BITS;
+    }
+    return l;
+  }
+  static constexpr L value = make();
+};
+
+template <class C>
+BH_DEV Fe<C> fe_zero() {
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) r.v[i] = 0;
+  return r;
+}
+
+template <class C>
+BH_DEV Fe<C> fe_one() {  // Montgomery form of 1
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) r.v[i] = C::ONE[i];
+  return r;
+}
+
+// Montgomery product, FIPS column order. Output < 2p (see header).
+template <class C>
+BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
+  constexpr int N = C::N;
+  Fe<C> r;
+  uint32_t m[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
+      acc += (uint64_t)m[i] * C::P[k - i];
+    if (k < N) {
+      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      acc += (uint64_t)m[k] * C::P[0];
+    } else {
+      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+    }
+    acc >>= BH_LIMB_BITS;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  return r;
+}
+
+// Montgomery square: cross products computed once against 2*a (limbs < 2^30).
+template <class C>
+BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
+  constexpr int N = C::N;
+  Fe<C> r;
+  uint32_t m[N], a2[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) a2[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    const int lo = (k < N ? 0 : k - N + 1);
+    const int hi = (k < N ? k : N - 1);
+#pragma unroll
+    for (int i = lo; i <= hi; i++) {
+      const int j = k - i;
+      if (i < j) acc += (uint64_t)a.v[i] * a2[j];
+      else if (i == j) acc += (uint64_t)a.v[i] * a.v[i];
+    }
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
+      acc += (uint64_t)m[i] * C::P[k - i];
+    if (k < N) {
+      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      acc += (uint64_t)m[k] * C::P[0];
+    } else {
+      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+    }
+    acc >>= BH_LIMB_BITS;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  return r;
+}
+
+// a + b (no modular reduction; caller tracks the bound)
+template <class C>
+BH_DEV Fe<C> fe_add(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    uint32_t s = a.v[i] + b.v[i] + c;
+    r.v[i] = s & BH_LIMB_MASK;
+    c = s >> BH_LIMB_BITS;
+  }
+  return r;
+}
+
+// a + K*p - b   (requires b < K*p)
+template <class C, uint32_t K>
+BH_DEV Fe<C> fe_sub(const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    int32_t s = (int32_t)(a.v[i] + KP<C, K>::value.v[i]) - (int32_t)b.v[i] + c;
+    r.v[i] = (uint32_t)s & BH_LIMB_MASK;
+    c = s >> BH_LIMB_BITS;  // arithmetic shift: -1, 0 or +1
+  }
+  return r;
+}
+
+// K*p - a (requires a < K*p)
+template <class C, uint32_t K>
+BH_DEV Fe<C> fe_neg(const Fe<C>& a) {
+  return fe_sub<C, K>(fe_zero<C>(), a);
+}
+
+// conditional subtraction: if x >= K*p then x - K*p
+template <class C, uint32_t K>
+BH_DEV Fe<C> fe_csub(const Fe<C>& x) {
+  Fe<C> t;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    int32_t s = (int32_t)x.v[i] - (int32_t)KP<C, K>::value.v[i] + c;
+    t.v[i] = (uint32_t)s & BH_LIMB_MASK;
+    c = s >> BH_LIMB_BITS;
+  }
+  const bool ge = (c >= 0);
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) r.v[i] = ge ? t.v[i] : x.v[i];
+  return r;
+}
+
+// Fully reduce x < 128p into [0, p).
+template <class C>
+BH_DEV Fe<C> fe_reduce_full(Fe<C> x) {
+  x = fe_csub<C, 64>(x);
+  x = fe_csub<C, 32>(x);
+  x = fe_csub<C, 16>(x);
+  x = fe_csub<C, 8>(x);
+  x = fe_csub<C, 4>(x);
+  x = fe_csub<C, 2>(x);
+  x = fe_csub<C, 1>(x);
+  return x;
+}
+
+// x ≡ 0 (mod p), valid for x < 128p.  x = k*p exactly when the low limb gives
+// k = x0 * p^-1 mod 2^29 < 128 and the full comparison with k*p succeeds.
+template <class C>
+BH_DEV bool fe_is_zero(const Fe<C>& x) {
+  const uint32_t k = (x.v[0] * C::P0INV) & BH_LIMB_MASK;
+  if (k >= 128u) return false;
+  uint64_t carry = 0;
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    uint64_t t = (uint64_t)C::P[i] * k + carry;
+    diff |= ((uint32_t)t & BH_LIMB_MASK) ^ x.v[i];
+    carry = t >> BH_LIMB_BITS;
+  }
+  return diff == 0;
+}
+
+template <class C>
+BH_DEV bool fe_is_zero_canonical(const Fe<C>& x) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) d |= x.v[i];
+  return d == 0;
+}
+
+template <class C>
+BH_DEV Fe<C> fe_select(bool c, const Fe<C>& a, const Fe<C>& b) {
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+
+// ---------------------------------------------------------------- packing
+// Packed storage: the (near-)canonical value in W = ceil(29N/32) - 0/1 32-bit words.
+// DFp packs into 12 words (value < 2^384), Fr into 8 words (value < 2^256).
+template <class C> struct Packed;
+template <> struct Packed<FpCfg> { static constexpr int W = 12; };
+template <> struct Packed<FrCfg> { static constexpr int W = 8; };
+
+template <class C>
+BH_DEV Fe<C> fe_unpack(const uint32_t* w) {
+  constexpr int W = Packed<C>::W;
+  Fe<C> r;
+#pragma unroll
+  for (int i = 0; i < C::N; i++) {
+    const int bit = i * BH_LIMB_BITS;
+    const int wi = bit >> 5, sh = bit & 31;
+    uint64_t lo = w[wi];
+    uint64_t hi = (wi + 1 < W) ? (uint64_t)w[wi + 1] : 0ull;
+    r.v[i] = (uint32_t)(((hi << 32) | lo) >> sh) & BH_LIMB_MASK;
+  }
+  return r;
+}
+
+// x must be < 2^(32W) (e.g. fully reduced)
+template <class C>
+BH_DEV void fe_pack(const Fe<C>& x, uint32_t* w) {
+  constexpr int W = Packed<C>::W;
+#pragma unroll
+  for (int j = 0; j < W; j++) {
+    uint64_t acc = 0;
+    const int bit0 = j * 32;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) {
+      const int b = i * BH_LIMB_BITS;
+      if (b + BH_LIMB_BITS <= bit0 || b >= bit0 + 32) continue;
+      if (b >= bit0) acc |= (uint64_t)x.v[i] << (b - bit0);
+      else acc |= (uint64_t)x.v[i] >> (bit0 - b);
+    }
+    w[j] = (uint32_t)acc;
+  }
+}
+
+// ---------------------------------------------------------------- DFp2 = DFp[u]/(u^2+1)
+struct DFp2 {
+  Fe<FpCfg> c0, c1;
+};
+
+using DFp = Fe<FpCfg>;
+using DFr = Fe<FrCfg>;
+
+// Field-generic wrappers so the curve code is written once for DFp (G1) and DFp2 (G2).
+// MB = bound (in multiples of p) of a product; is_zero valid below 128p.
+struct FpOps {
+  using T = DFp;
+  static constexpr uint32_t MB = 2;
+  static BH_DEV T mul(const T& a, const T& b) { return fe_mul<FpCfg>(a, b); }
+  static BH_DEV T sqr(const T& a) { return fe_sqr<FpCfg>(a); }
+  static BH_DEV T add(const T& a, const T& b) { return fe_add<FpCfg>(a, b); }
+  template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) { return fe_sub<FpCfg, K>(a, b); }
+  static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a); }
+  static BH_DEV T zero() { return fe_zero<FpCfg>(); }
+  static BH_DEV T one() { return fe_one<FpCfg>(); }
+  static BH_DEV T reduce(const T& a) { return fe_reduce_full<FpCfg>(a); }
+  static BH_DEV T neg_canonical(const T& a) {  // p - a for a in [0,p], result in [0,p]
+    return fe_csub<FpCfg, 1>(fe_sub<FpCfg, 1>(fe_zero<FpCfg>(), a));
+  }
+  static BH_DEV T select(bool c, const T& a, const T& b) { return fe_select<FpCfg>(c, a, b); }
+  static constexpr int PACKED_WORDS = 12;
+  static BH_DEV T unpack(const uint32_t* w) { return fe_unpack<FpCfg>(w); }
+  static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<FpCfg>(a, w); }
+};
+
+struct Fp2Ops {
+  using T = DFp2;
+  static constexpr uint32_t MB = 6;
+  static BH_DEV T mul(const T& a, const T& b) {
+    DFp t0 = fe_mul<FpCfg>(a.c0, b.c0);
+    DFp t1 = fe_mul<FpCfg>(a.c1, b.c1);
+    DFp t2 = fe_mul<FpCfg>(fe_add<FpCfg>(a.c0, a.c1), fe_add<FpCfg>(b.c0, b.c1));
+    T r;
+    r.c0 = fe_sub<FpCfg, 2>(t0, t1);                       // < 4p
+    r.c1 = fe_sub<FpCfg, 4>(t2, fe_add<FpCfg>(t0, t1));     // < 6p
+    return r;
+  }
+  static BH_DEV T sqr(const T& a) {
+    T r;
+    // (a0 + a1)(a0 - a1), 2 a0 a1 ; valid for inputs < 128p
+    r.c0 = fe_mul<FpCfg>(fe_add<FpCfg>(a.c0, a.c1), fe_sub<FpCfg, 128>(a.c0, a.c1));
+    DFp t = fe_mul<FpCfg>(a.c0, a.c1);
+    r.c1 = fe_add<FpCfg>(t, t);                              // < 4p
+    return r;
+  }
+  static BH_DEV T add(const T& a, const T& b) {
+    return T{fe_add<FpCfg>(a.c0, b.c0), fe_add<FpCfg>(a.c1, b.c1)};
+  }
+  template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) {
+    return T{fe_sub<FpCfg, K>(a.c0, b.c0), fe_sub<FpCfg, K>(a.c1, b.c1)};
+  }
+  static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a.c0) && fe_is_zero<FpCfg>(a.c1); }
+  static BH_DEV T zero() { return T{fe_zero<FpCfg>(), fe_zero<FpCfg>()}; }
+  static BH_DEV T one() { return T{fe_one<FpCfg>(), fe_zero<FpCfg>()}; }
+  static BH_DEV T reduce(const T& a) { return T{fe_reduce_full<FpCfg>(a.c0), fe_reduce_full<FpCfg>(a.c1)}; }
+  static BH_DEV T neg_canonical(const T& a) { return T{FpOps::neg_canonical(a.c0), FpOps::neg_canonical(a.c1)}; }
+  static BH_DEV T select(bool c, const T& a, const T& b) {
+    return T{fe_select<FpCfg>(c, a.c0, b.c0), fe_select<FpCfg>(c, a.c1, b.c1)};
+  }
+  static constexpr int PACKED_WORDS = 24;  // c0 then c1
+  static BH_DEV T unpack(const uint32_t* w) { return T{fe_unpack<FpCfg>(w), fe_unpack<FpCfg>(w + 12)}; }
+  static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<FpCfg>(a.c0, w); fe_pack<FpCfg>(a.c1, w + 12); }
+};

@@ -1,0 +1,59 @@
+// Host interface of the device Pippenger MSM (msm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include "curve.cuh"
+
+namespace bh {
+
+struct MsmShape {
+  int c;   // window bits
+  int W;   // windows = ceil(256 / c) (signed digits need one spare bit)
+  int NB;  // buckets per window = 2^(c-1)
+  int L;   // buckets per running-sum thread
+  int S;   // sorted entries per accumulation thread
+};
+MsmShape msm_shape(size_t n, int c_override);
+
+struct MsmTiming {
+  hipEvent_t ev_acc_begin = nullptr, ev_acc_end = nullptr;  // bracket k_accumulate_dev
+};
+
+template <class C>
+struct MsmWorkspace {
+  size_t cap_n = 0, cap_E = 0, cap_nbt = 0, cap_segs = 0, cap_T = 0;
+  uint32_t *entries = nullptr, *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *scan_scratch = nullptr;
+  typename C::P *bucket_sums = nullptr, *conts = nullptr, *seg_weighted = nullptr, *seg_sum = nullptr,
+                *window_sums = nullptr;
+  typename C::P* host_window_sums = nullptr;  // pinned, W entries after the stream completes
+  static size_t bytes_needed(size_t n);
+  hipError_t reserve(size_t n_max);                         // every automatic shape up to n_max
+  hipError_t reserve_shape(size_t n, const MsmShape& sh);    // grow (never shrink) for one shape
+  hipError_t grow(size_t E, size_t nbt, size_t segs, size_t T);
+  void release();
+};
+
+// Enqueue an MSM on `st`; on completion ws.host_window_sums[0..W) hold the
+// canonical XYZZ sum of every window (device Montgomery form).
+// d_scalars: n canonical scalars (8 LE u32 words each); d_idx: per-scalar base
+// index (-1 = density bit clear) or nullptr for idx = base_offset + i.
+template <class C>
+hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                           size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
+                           MsmTiming* timing);
+
+size_t scan_scratch_words(size_t n);
+void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st);
+hipError_t scalars_prepare(const uint32_t* d_in, uint32_t* d_out, size_t n, int mode, int log_perm, hipStream_t st);
+hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset, int32_t* d_idx, uint32_t* d_tmp,
+                         uint32_t* d_scan_scratch, hipStream_t st);
+
+}  // namespace bh
+
+namespace bh {
+hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, const MsmShape& sh,
+                       uint32_t* counts, hipStream_t st);
+hipError_t launch_scatter(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
+                          const MsmShape& sh, uint32_t* cursor, uint32_t* entries, hipStream_t st);
+}  // namespace bh

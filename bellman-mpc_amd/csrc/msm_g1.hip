@@ -1,0 +1,8 @@
+// G1Ops instantiation of the device MSM (see msm_impl.cuh).
+#include "msm_impl.cuh"
+
+namespace bh {
+template struct MsmWorkspace<G1Ops>;
+template hipError_t msm_window_sums<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
+                                         const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
+}  // namespace bh

@@ -1,0 +1,8 @@
+// G2Ops instantiation of the device MSM (see msm_impl.cuh).
+#include "msm_impl.cuh"
+
+namespace bh {
+template struct MsmWorkspace<G2Ops>;
+template hipError_t msm_window_sums<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
+                                         const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
+}  // namespace bh

@@ -1,0 +1,295 @@
+// Curve-generic MSM kernels and host driver (included once per curve by
+// msm_g1.hip / msm_g2.hip so the two instantiations compile in parallel).
+#pragma once
+#include "msm.h"
+#include <algorithm>
+
+namespace bh {
+
+static inline unsigned msm_blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// ----------------------------------------------------------------- accumulate
+template <class C>
+__device__ __forceinline__ typename C::A load_base(const uint32_t* bases, uint32_t e) {
+  using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+  constexpr int PW = F::PACKED_WORDS;
+  const uint32_t idx = e & 0x7fffffffu;
+  const uint4* p = reinterpret_cast<const uint4*>(bases + (size_t)idx * 2 * PW);
+  uint32_t w[2 * PW];
+#pragma unroll
+  for (int k = 0; k < PW / 2; k++) {
+    uint4 v = p[k];
+    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+  }
+  typename C::A a;
+  a.x = F::unpack(w);
+  a.y = F::unpack(w + PW);
+  if (e & 0x80000000u) a = C::neg_affine(a);
+  return a;
+}
+
+template <class C>
+__device__ __forceinline__ void store_point(typename C::P* dst, const typename C::P& p) {
+  constexpr int WORDS = sizeof(typename C::P) / 16;
+  const uint4* s = reinterpret_cast<const uint4*>(&p);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int k = 0; k < WORDS; k++) d[k] = s[k];
+}
+template <class C>
+__device__ __forceinline__ typename C::P load_point(const typename C::P* src) {
+  typename C::P p;
+  constexpr int WORDS = sizeof(typename C::P) / 16;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(&p);
+#pragma unroll
+  for (int k = 0; k < WORDS; k++) d[k] = s[k];
+  return p;
+}
+
+// largest b in [0, nb) with offsets[b] <= pos  (offsets has nb+1 entries, offsets[nb] > pos)
+__device__ __forceinline__ uint32_t find_bucket(const uint32_t* offsets, uint32_t nb, uint32_t pos) {
+  uint32_t lo = 0, hi = nb;  // invariant offsets[lo] <= pos < offsets[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (offsets[mid] <= pos) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// full sum of bucket gb (0..nbt): own partial + continuation partials
+template <class C>
+__device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_t* counts, const uint32_t* offsets,
+                                                      const typename C::P* bucket_sums, const typename C::P* conts,
+                                                      uint32_t S) {
+  const uint32_t cnt = counts[gb];
+  if (cnt == 0) return C::identity();
+  typename C::P v = load_point<C>(&bucket_sums[gb]);
+  const uint32_t off = offsets[gb];
+  const uint32_t s_first = off / S, s_last = (off + cnt - 1) / S;
+  for (uint32_t s = s_first + 1; s <= s_last; s++) v = C::add(v, load_point<C>(&conts[s]));
+  return v;
+}
+
+// thread (w, t): buckets [t*L, (t+1)*L) of window w
+template <class C>
+__global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t* counts, const uint32_t* offsets,
+                                                       const typename C::P* bucket_sums, const typename C::P* conts,
+                                                       uint32_t S, uint32_t NB, uint32_t L, uint32_t W,
+                                                       typename C::P* seg_weighted, typename C::P* seg_sum) {
+  const uint32_t T = NB / L;
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= W * T) return;
+  const uint32_t w = gid / T, t = gid % T;
+  typename C::P running = C::identity(), acc = C::identity();
+  for (int k = (int)L - 1; k >= 0; k--) {
+    const uint32_t gb = w * NB + t * L + (uint32_t)k;
+    running = C::add(running, bucket_value<C>(gb, counts, offsets, bucket_sums, conts, S));
+    acc = C::add(acc, running);
+  }
+  store_point<C>(&seg_weighted[gid], acc);
+  store_point<C>(&seg_sum[gid], running);
+}
+
+// v_t = weighted_t + (t*L) * sum_t
+template <class C>
+__global__ void __launch_bounds__(256) k_seg_combine(typename C::P* seg_weighted, const typename C::P* seg_sum,
+                                                     uint32_t T, uint32_t L, uint32_t total) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint32_t k = (gid % T) * L;
+  typename C::P v = load_point<C>(&seg_weighted[gid]);
+  if (k != 0) {
+    const typename C::P base = load_point<C>(&seg_sum[gid]);
+    typename C::P m = C::identity();
+    for (int bit = 31 - __clz(k); bit >= 0; bit--) {
+      m = C::dbl(m);
+      if ((k >> bit) & 1u) m = C::add(m, base);
+    }
+    v = C::add(v, m);
+  }
+  store_point<C>(&seg_weighted[gid], v);
+}
+
+// one block per window: sum T points -> window_out[w] (canonical coordinates)
+template <class C, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_tree_reduce(const typename C::P* pts, uint32_t T, typename C::P* window_out) {
+  __shared__ typename C::P sh[BLOCK];
+  const uint32_t w = blockIdx.x;
+  typename C::P acc = C::identity();
+  for (uint32_t t = threadIdx.x; t < T; t += BLOCK) acc = C::add(acc, load_point<C>(&pts[(size_t)w * T + t]));
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = BLOCK / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) sh[threadIdx.x] = C::add(sh[threadIdx.x], sh[threadIdx.x + off]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) window_out[w] = C::reduce(sh[0]);
+}
+
+// The accumulate kernel needs E; it reads it from offsets[nbt] on device.
+template <class C>
+__global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
+                                                        const uint32_t* bases, uint32_t S,
+                                                        typename C::P* bucket_sums, typename C::P* conts) {
+  const uint32_t E = offsets[nbt];
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pos0 = seg * S;
+  if (pos0 >= E) return;
+  const uint32_t end = min(pos0 + S, E);
+  uint32_t b = find_bucket(offsets, nbt, pos0);
+  uint32_t next = offsets[b + 1];
+  bool started_here = offsets[b] >= pos0;
+  typename C::P acc = C::identity();
+  for (uint32_t j = pos0; j < end; j++) {
+    if (j == next) {
+      if (started_here) store_point<C>(&bucket_sums[b], acc);
+      else store_point<C>(&conts[seg], acc);
+      b++;
+      while (offsets[b + 1] <= j) b++;
+      next = offsets[b + 1];
+      started_here = true;
+      acc = C::identity();
+    }
+    const typename C::A a = load_base<C>(bases, entries[j]);
+    acc = C::madd(acc, a);
+  }
+  if (started_here) store_point<C>(&bucket_sums[b], acc);
+  else store_point<C>(&conts[seg], acc);
+}
+
+template <class C>
+size_t MsmWorkspace<C>::bytes_needed(size_t n) {
+  MsmShape sh = msm_shape(n, 0);
+  size_t E = n * (size_t)sh.W;
+  size_t nbt = (size_t)sh.W * sh.NB;
+  size_t segs = (E + sh.S - 1) / sh.S + 1;
+  size_t T = (size_t)sh.W * (sh.NB / sh.L);
+  return E * 4 + nbt * 4 * 3 + 16 + nbt * sizeof(typename C::P) + segs * sizeof(typename C::P) +
+         2 * T * sizeof(typename C::P) + n * 4;
+}
+
+template <class C>
+hipError_t MsmWorkspace<C>::grow(size_t E, size_t nbt, size_t segs, size_t T) {
+  hipError_t err;
+  if (E > cap_E) {
+    if (entries) hipFree(entries);
+    entries = nullptr;
+    if ((err = hipMalloc(&entries, std::max<size_t>(E, 1) * 4)) != hipSuccess) return err;
+    cap_E = E;
+  }
+  if (nbt > cap_nbt) {
+    if (counts) hipFree(counts);
+    if (offsets) hipFree(offsets);
+    if (cursor) hipFree(cursor);
+    if (scan_scratch) hipFree(scan_scratch);
+    if (bucket_sums) hipFree(bucket_sums);
+    counts = offsets = cursor = scan_scratch = nullptr;
+    bucket_sums = nullptr;
+    if ((err = hipMalloc(&counts, (nbt + 1) * 4)) != hipSuccess) return err;
+    if ((err = hipMalloc(&offsets, (nbt + 1) * 4)) != hipSuccess) return err;
+    if ((err = hipMalloc(&cursor, (nbt + 1) * 4)) != hipSuccess) return err;
+    if ((err = hipMalloc(&scan_scratch, scan_scratch_words(nbt + 1) * 4 + 64)) != hipSuccess) return err;
+    if ((err = hipMalloc(&bucket_sums, nbt * sizeof(typename C::P))) != hipSuccess) return err;
+    cap_nbt = nbt;
+  }
+  if (segs > cap_segs) {
+    if (conts) hipFree(conts);
+    conts = nullptr;
+    if ((err = hipMalloc(&conts, segs * sizeof(typename C::P))) != hipSuccess) return err;
+    cap_segs = segs;
+  }
+  if (T > cap_T) {
+    if (seg_weighted) hipFree(seg_weighted);
+    if (seg_sum) hipFree(seg_sum);
+    seg_weighted = seg_sum = nullptr;
+    if ((err = hipMalloc(&seg_weighted, T * sizeof(typename C::P))) != hipSuccess) return err;
+    if ((err = hipMalloc(&seg_sum, T * sizeof(typename C::P))) != hipSuccess) return err;
+    cap_T = T;
+  }
+  if (!window_sums) {
+    if ((err = hipMalloc(&window_sums, 256 * sizeof(typename C::P))) != hipSuccess) return err;
+    if ((err = hipHostMalloc(&host_window_sums, 256 * sizeof(typename C::P), hipHostMallocDefault)) != hipSuccess)
+      return err;
+  }
+  return hipSuccess;
+}
+
+template <class C>
+hipError_t MsmWorkspace<C>::reserve_shape(size_t n, const MsmShape& sh) {
+  const size_t E = n * (size_t)sh.W;
+  const size_t nbt = (size_t)sh.W * sh.NB;
+  const size_t segs = (E + sh.S - 1) / sh.S + 1;
+  const size_t T = (size_t)sh.W * (sh.NB / sh.L);
+  return grow(E, nbt, segs, T);
+}
+
+// size for every automatic shape up to n_max
+template <class C>
+hipError_t MsmWorkspace<C>::reserve(size_t n_max) {
+  for (size_t n = 1;; n <<= 1) {
+    size_t nn = std::min(n, n_max);
+    hipError_t e = reserve_shape(nn, msm_shape(nn, 0));
+    if (e != hipSuccess) return e;
+    if (nn == n_max) break;
+  }
+  if (n_max > cap_n) cap_n = n_max;
+  return hipSuccess;
+}
+
+template <class C>
+void MsmWorkspace<C>::release() {
+  if (entries) hipFree(entries);
+  if (counts) hipFree(counts);
+  if (offsets) hipFree(offsets);
+  if (cursor) hipFree(cursor);
+  if (scan_scratch) hipFree(scan_scratch);
+  if (bucket_sums) hipFree(bucket_sums);
+  if (conts) hipFree(conts);
+  if (seg_weighted) hipFree(seg_weighted);
+  if (seg_sum) hipFree(seg_sum);
+  if (window_sums) hipFree(window_sums);
+  if (host_window_sums) hipHostFree(host_window_sums);
+  entries = counts = offsets = cursor = scan_scratch = nullptr;
+  bucket_sums = conts = seg_weighted = seg_sum = window_sums = nullptr;
+  host_window_sums = nullptr;
+  cap_n = cap_E = cap_nbt = cap_segs = cap_T = 0;
+}
+
+template <class C>
+hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                           size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
+                           MsmTiming* timing) {
+  {
+    hipError_t e = ws.reserve_shape(n, sh);
+    if (e != hipSuccess) return e;
+  }
+  const size_t nbt = (size_t)sh.W * sh.NB;
+  hipMemsetAsync(ws.counts, 0, (nbt + 1) * 4, st);
+  launch_hist(d_scalars, n, d_idx, sh, ws.counts, st);
+  exclusive_scan(ws.counts, ws.offsets, nbt + 1, ws.scan_scratch, st);
+  hipMemcpyAsync(ws.cursor, ws.offsets, (nbt + 1) * 4, hipMemcpyDeviceToDevice, st);
+  if (n > 0) {
+    launch_scatter(d_scalars, n, d_idx, base_offset, sh, ws.cursor, ws.entries, st);
+    const size_t Emax = n * (size_t)sh.W;
+    const size_t segs = (Emax + sh.S - 1) / sh.S;
+    if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
+    hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries, ws.offsets,
+                       (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts);
+    if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
+  }
+  const uint32_t T = (uint32_t)(sh.NB / sh.L);
+  const size_t total = (size_t)sh.W * T;
+  hipLaunchKernelGGL(k_bucket_reduce<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
+                     ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, (uint32_t)sh.L, (uint32_t)sh.W,
+                     ws.seg_weighted, ws.seg_sum);
+  hipLaunchKernelGGL(k_seg_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.seg_weighted, ws.seg_sum, T,
+                     (uint32_t)sh.L, (uint32_t)total);
+  constexpr int TB = std::is_same<C, G1Ops>::value ? 128 : 64;
+  hipLaunchKernelGGL((k_tree_reduce<C, TB>), dim3(sh.W), dim3(TB), 0, st, ws.seg_weighted, T, ws.window_sums);
+  hipMemcpyAsync(ws.host_window_sums, ws.window_sums, sh.W * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+  return hipGetLastError();
+}
+
+}  // namespace bh

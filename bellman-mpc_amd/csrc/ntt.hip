@@ -1,0 +1,268 @@
+// Radix-2 NTT family over BLS12-381 DFr on gfx950 -- the device replacement for
+// EvaluationDomain (reference src/domain.rs:42-190) and its best_fft /
+// serial_fft / parallel_fft (domain.rs:261-372).
+//
+// Storage: every DFr value is 8 packed u32 words holding x*2^261 mod r (device
+// Montgomery form), kept < 2r.  A transform is ceil(log m / 10) passes; each
+// pass stages 1024 elements of one workgroup in LDS (9 limb planes, 36 KB),
+// runs up to 10 radix-2 stages there and writes back:
+//   DIF (Gentleman-Sande): natural order in  -> bit-reversed order out
+//   DIT (Cooley-Tukey)   : bit-reversed in   -> natural order out
+// The reference's natural->natural fft is therefore `permute + DIT`, and the
+// Groth16 H pipeline (prover.rs:210-231) runs DIF for every inverse transform
+// and DIT for every forward one, so no permutation pass is ever needed there;
+// the coset factors g^i (distribute_powers, domain.rs:101-113), m^-1
+// (domain.rs:88-98) and 1/Z(g) (domain.rs:139-151) are fused into the pass
+// that stores the data, indexed by the element's natural index.
+#include "ntt.h"
+
+namespace bh {
+
+static constexpr int NTT_E = 1024;  // elements per workgroup
+static constexpr int NTT_T = 256;   // threads per workgroup
+
+__device__ __forceinline__ DFr ld_packed(const uint32_t* a, size_t i) {
+  const uint4* p = reinterpret_cast<const uint4*>(a + i * 8);
+  uint4 x = p[0], y = p[1];
+  uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  return fe_unpack<FrCfg>(w);
+}
+__device__ __forceinline__ void st_packed(uint32_t* a, size_t i, const DFr& v) {
+  uint32_t w[8];
+  fe_pack<FrCfg>(v, w);
+  uint4* p = reinterpret_cast<uint4*>(a + i * 8);
+  p[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  p[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+__device__ __forceinline__ DFr ld_limbs(const uint32_t* t, size_t i) {  // unpacked table entry (9 words)
+  DFr r;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.v[k] = t[i * 9 + k];
+  return r;
+}
+__device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
+  return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0u;
+}
+// factor(i) = lo[i & (2^lo_bits-1)] * hi[i >> lo_bits]   (tables unpacked)
+// lo_bits < 0: constant factor hi[0]
+__device__ __forceinline__ DFr pow_factor(const uint32_t* lo, const uint32_t* hi, int lo_bits, uint32_t i) {
+  if (lo_bits < 0) return ld_limbs(hi, 0);
+  return fe_mul<FrCfg>(ld_limbs(lo, i & ((1u << lo_bits) - 1u)), ld_limbs(hi, i >> lo_bits));
+}
+
+struct PassArgs {
+  int L, t, D;
+  const uint32_t* tw;     // omega^j, j < m/2 (unpacked)
+  const uint32_t* post_lo;  // optional post-scale tables
+  const uint32_t* post_hi;
+  int post_lo_bits;
+};
+
+// global element index of (group g, position k) for a DIF pass at stages t..t+D-1
+__device__ __forceinline__ uint32_t dif_index(const PassArgs& a, uint32_t g, uint32_t k) {
+  const uint32_t s = 1u << (a.L - a.t - a.D);
+  const uint32_t lo = g & (s - 1), hi = g >> (a.L - a.t - a.D);
+  return (hi << (a.L - a.t)) + k * s + lo;
+}
+// ... for a DIT pass at stages t..t+D-1 (half sizes 2^t .. 2^(t+D-1))
+__device__ __forceinline__ uint32_t dit_index(const PassArgs& a, uint32_t g, uint32_t k) {
+  const uint32_t lo = g & ((1u << a.t) - 1), hi = g >> a.t;
+  return (hi << (a.t + a.D)) + (k << a.t) + lo;
+}
+
+template <bool DIF>
+__global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) {
+  __shared__ uint32_t lds[9 * NTT_E];
+  const int D = a.D;
+  const uint32_t G = NTT_E >> D;             // groups per workgroup
+  const uint32_t total_groups = 1u << (a.L - D);
+  const uint32_t g0 = blockIdx.x * G;
+  const uint32_t stride = DIF ? (1u << (a.L - a.t - D)) : (1u << a.t);  // distance between consecutive lo's
+  const bool lo_fast = stride >= G;  // coalesce along lo (groups) or along k
+  const uint32_t K = 1u << D;
+  // ---- load
+  for (uint32_t e = threadIdx.x; e < (uint32_t)NTT_E; e += NTT_T) {
+    uint32_t gl, k;
+    if (lo_fast) { gl = e % G; k = e / G; } else { k = e & (K - 1); gl = e >> D; }
+    const uint32_t g = g0 + gl;
+    if (g >= total_groups) continue;
+    const uint32_t idx = DIF ? dif_index(a, g, k) : dit_index(a, g, k);
+    DFr x = ld_packed(data, idx);
+    const uint32_t slot = k * G + gl;
+#pragma unroll
+    for (int l = 0; l < 9; l++) lds[l * NTT_E + slot] = x.v[l];
+  }
+  __syncthreads();
+  // ---- D radix-2 stages
+  for (int j = 0; j < D; j++) {
+    const int u = a.t + j;  // global stage
+    for (uint32_t b = threadIdx.x; b < (uint32_t)(NTT_E / 2); b += NTT_T) {
+      const uint32_t gl = b % G, r = b / G;
+      if (g0 + gl >= total_groups) continue;
+      const int hb = DIF ? (D - 1 - j) : j;  // pair distance 2^hb in k
+      const uint32_t k = ((r >> hb) << (hb + 1)) | (r & ((1u << hb) - 1));
+      const uint32_t k2 = k + (1u << hb);
+      const uint32_t s0 = k * G + gl, s1 = k2 * G + gl;
+      DFr x, y;
+#pragma unroll
+      for (int l = 0; l < 9; l++) { x.v[l] = lds[l * NTT_E + s0]; y.v[l] = lds[l * NTT_E + s1]; }
+      const uint32_t g = g0 + gl;
+      uint32_t e;
+      if (DIF) {
+        const uint32_t s = 1u << (a.L - a.t - D);
+        const uint32_t lo = g & (s - 1);
+        e = (((k & ((1u << hb) - 1)) * s) + lo) << u;
+      } else {
+        const uint32_t lo = g & ((1u << a.t) - 1);
+        e = (((k & ((1u << hb) - 1)) << a.t) + lo) << (a.L - u - 1);
+      }
+      const DFr w = ld_limbs(a.tw, e);
+      DFr nx, ny;
+      if (DIF) {
+        nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
+        ny = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x, y), w);
+      } else {
+        const DFr t = fe_mul<FrCfg>(y, w);
+        nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, t));
+        ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, t));
+      }
+#pragma unroll
+      for (int l = 0; l < 9; l++) { lds[l * NTT_E + s0] = nx.v[l]; lds[l * NTT_E + s1] = ny.v[l]; }
+    }
+    __syncthreads();
+  }
+  // ---- store (+ optional post-scale by natural index)
+  for (uint32_t e = threadIdx.x; e < (uint32_t)NTT_E; e += NTT_T) {
+    uint32_t gl, k;
+    if (lo_fast) { gl = e % G; k = e / G; } else { k = e & (K - 1); gl = e >> D; }
+    const uint32_t g = g0 + gl;
+    if (g >= total_groups) continue;
+    const uint32_t idx = DIF ? dif_index(a, g, k) : dit_index(a, g, k);
+    const uint32_t slot = k * G + gl;
+    DFr x;
+#pragma unroll
+    for (int l = 0; l < 9; l++) x.v[l] = lds[l * NTT_E + slot];
+    if (a.post_hi) {
+      const uint32_t nat = DIF ? brev(idx, a.L) : idx;
+      x = fe_mul<FrCfg>(x, pow_factor(a.post_lo, a.post_hi, a.post_lo_bits, nat));
+    }
+    st_packed(data, idx, x);
+  }
+}
+
+// out[bitrev(i)] = in[i] * factor(i)   (factor optional)
+__global__ void __launch_bounds__(256) k_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo,
+                                                 const uint32_t* hi, int lo_bits) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1u << L)) return;
+  DFr x = ld_packed(in, i);
+  if (hi) x = fe_mul<FrCfg>(x, pow_factor(lo, hi, lo_bits, i));
+  st_packed(out, brev(i, L), x);
+}
+
+// a[i] *= factor(i)  or a[i] *= c (constant, unpacked) when lo == nullptr
+__global__ void __launch_bounds__(256) k_scale(uint32_t* a, uint32_t n, const uint32_t* lo, const uint32_t* hi,
+                                               int lo_bits, const uint32_t* c) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DFr x = ld_packed(a, i);
+  const DFr f = hi ? pow_factor(lo, hi, lo_bits, i) : ld_limbs(c, 0);
+  st_packed(a, i, fe_mul<FrCfg>(x, f));
+}
+
+// op 0: a *= b ; op 1: a -= b ; op 2: out = (a*b - c) * k   (H pipeline, prover.rs:221-225)
+__global__ void __launch_bounds__(256) k_pointwise(uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t n,
+                                                   int op, const uint32_t* k) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DFr x = ld_packed(a, i), y = ld_packed(b, i);
+  DFr r;
+  if (op == 0) r = fe_mul<FrCfg>(x, y);
+  else if (op == 1) r = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, y));
+  else {
+    DFr z = ld_packed(c, i);
+    r = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(fe_mul<FrCfg>(x, y), z), ld_limbs(k, 0));
+  }
+  st_packed(a, i, r);
+}
+
+// format conversion: out = in * C (C raw unpacked, 9 limbs) [* reduce to canonical]
+__global__ void __launch_bounds__(256) k_fr_convert(const uint32_t* in, uint32_t* out, uint32_t n, FrConst C,
+                                                    int reduce) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DFr x = ld_packed(in, i);
+  DFr c;
+#pragma unroll
+  for (int l = 0; l < 9; l++) c.v[l] = C.v[l];
+  DFr r = fe_mul<FrCfg>(x, c);
+  if (reduce) r = fe_reduce_full<FrCfg>(r);
+  st_packed(out, i, r);
+}
+
+// tab[j] = lo[j & mask] * hi[j >> bits] for j < n  (builds twiddle tables on device)
+__global__ void __launch_bounds__(256) k_expand_table(uint32_t* tab, uint32_t n, const uint32_t* lo,
+                                                      const uint32_t* hi, int lo_bits) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  DFr x = pow_factor(lo, hi, lo_bits, j);
+  x = fe_csub<FrCfg, 1>(x);
+#pragma unroll
+  for (int l = 0; l < 9; l++) tab[(size_t)j * 9 + l] = x.v[l];
+}
+
+// ------------------------------------------------------------------ host side
+static inline unsigned nb(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* tw, const uint32_t* post_lo, const uint32_t* post_hi,
+                int post_lo_bits, hipStream_t st) {
+  if (L == 0) {
+    if (post_hi) hipLaunchKernelGGL(k_scale, dim3(1), dim3(256), 0, st, d, 1u, post_lo, post_hi, post_lo_bits,
+                                    (const uint32_t*)nullptr);
+    return;
+  }
+  const int passes = (L + 9) / 10;
+  int Ds[8];
+  for (int p = 0; p < passes; p++) Ds[p] = L / passes + (p < L % passes ? 1 : 0);
+  int t = 0;
+  for (int p = 0; p < passes; p++) {
+    PassArgs a;
+    a.L = L; a.t = t; a.D = Ds[p]; a.tw = tw;
+    const bool last = (p == passes - 1);
+    a.post_lo = last ? post_lo : nullptr;
+    a.post_hi = last ? post_hi : nullptr;
+    a.post_lo_bits = post_lo_bits;
+    const size_t groups = (size_t)1 << (L - a.D);
+    const size_t G = NTT_E >> a.D;
+    const unsigned blocks = (unsigned)((groups + G - 1) / G);
+    if (dif) hipLaunchKernelGGL(k_ntt_pass<true>, dim3(blocks), dim3(NTT_T), 0, st, d, a);
+    else hipLaunchKernelGGL(k_ntt_pass<false>, dim3(blocks), dim3(NTT_T), 0, st, d, a);
+    t += a.D;
+  }
+}
+
+void launch_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo, const uint32_t* hi, int lo_bits,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(k_permute, dim3(nb((size_t)1 << L, 256)), dim3(256), 0, st, in, out, L, lo, hi, lo_bits);
+}
+void launch_scale(uint32_t* a, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits, const uint32_t* c,
+                  hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_scale, dim3(nb(n, 256)), dim3(256), 0, st, a, (uint32_t)n, lo, hi, lo_bits, c);
+}
+void launch_pointwise(uint32_t* a, const uint32_t* b, const uint32_t* c, size_t n, int op, const uint32_t* k,
+                      hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_pointwise, dim3(nb(n, 256)), dim3(256), 0, st, a, b, c, (uint32_t)n, op, k);
+}
+void launch_fr_convert(const uint32_t* in, uint32_t* out, size_t n, const FrConst& C, int reduce, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fr_convert, dim3(nb(n, 256)), dim3(256), 0, st, in, out, (uint32_t)n, C, reduce);
+}
+void launch_expand_table(uint32_t* tab, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits,
+                         hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_expand_table, dim3(nb(n, 256)), dim3(256), 0, st, tab, (uint32_t)n, lo, hi, lo_bits);
+}
+
+}  // namespace bh

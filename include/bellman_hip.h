@@ -1,0 +1,148 @@
+/*
+ * bellman_hip.h -- C ABI of the MI355X-native Groth16 prover core.
+ *
+ * Drop-in boundary for the data-parallel hot path of doubiliu/bellman-mpc
+ * (a fork of zkcrypto bellman 0.11.1).  Every entry point names the reference
+ * interface it replaces (paths relative to bellman/src in the reference):
+ *
+ *   bh_multiexp            multiexp::multiexp            multiexp.rs:252-281
+ *   bh_srs_upload          (Arc<Vec<G>>, usize) SourceBuilder / Parameters::read
+ *                                                         multiexp.rs:45-86, groth16/mod.rs:292-400
+ *   bh_fft / bh_ifft / bh_coset_fft / bh_icoset_fft /
+ *   bh_distribute_powers / bh_divide_by_z_on_coset /
+ *   bh_mul_assign / bh_sub_assign
+ *                          EvaluationDomain methods      domain.rs:81-189
+ *   bh_domain_size         EvaluationDomain::from_coeffs  domain.rs:47-79
+ *   bh_compute_h           the H block of create_proof   groth16/prover.rs:210-231
+ *   bh_params_*            Parameters / ParameterSource  groth16/mod.rs:224-477
+ *   bh_prove / bh_prove_witness
+ *                          create_proof after synthesis   groth16/prover.rs:206-349
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; the caller owns every host buffer and the
+ *     library never retains a caller pointer after a call returns.
+ *   - Fr vectors ("Montgomery") use the bls12_381 0.6 in-memory layout:
+ *     4 little-endian u64 limbs of x * 2^256 mod r per element.
+ *   - Exponents for bh_multiexp are Scalar::to_le_bits() words (canonical,
+ *     4 LE u64 per scalar) unless BH_SCALARS_MONTGOMERY is given.
+ *   - Density maps are bitvec<u64, Lsb0> words: bit i of word i/64 is entry i.
+ *   - Group elements use the zcash/bls12_381 encodings (big-endian, flag bits
+ *     in byte 0): uncompressed 96 B (G1) / 192 B (G2), compressed 48/96 B.
+ *   - Every function returns a bh_status; it never aborts across the FFI.
+ */
+#ifndef BELLMAN_HIP_H
+#define BELLMAN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes mirror SynthesisError (lib.rs:355-364). */
+typedef int bh_status;
+#define BH_OK 0
+#define BH_ERR_UNEXPECTED_IDENTITY 1     /* multiexp.rs:63-65, prover.rs:309-313 */
+#define BH_ERR_UNEXPECTED_EOF 2          /* IoError(UnexpectedEof), multiexp.rs:55-61,74-80 */
+#define BH_ERR_POLY_DEGREE_TOO_LARGE 3   /* domain.rs:57-59 */
+#define BH_ERR_DENSITY_SIZE_MISMATCH 4   /* the reference panics (assert), multiexp.rs:277 */
+#define BH_ERR_UNCONSTRAINED_VARIABLE 5  /* generator.rs:582-586 */
+#define BH_ERR_INVALID_ARGUMENT 10
+#define BH_ERR_INVALID_ENCODING 11       /* IoError(InvalidData) of Parameters::read */
+#define BH_ERR_NOT_ON_CURVE 12
+#define BH_ERR_OUT_OF_MEMORY 13
+#define BH_ERR_HIP 100                   /* HIP runtime / device failure */
+
+#define BH_G1 1
+#define BH_G2 2
+
+#define BH_SCALARS_CANONICAL 0
+#define BH_SCALARS_MONTGOMERY 1
+
+typedef struct bh_ctx bh_ctx;         /* one MI355X device + streams + workspaces (multicore.rs Worker) */
+typedef struct bh_srs bh_srs;         /* device-resident affine base vector */
+typedef struct bh_params bh_params;   /* device-resident Groth16 Parameters */
+typedef struct bh_witness bh_witness; /* device-resident complete assignment */
+
+const char* bh_status_string(bh_status s);
+int bh_version(void);
+
+/* ---- context (replaces multicore::Worker, multicore.rs:21-130) */
+bh_status bh_ctx_create(int device, bh_ctx** out);
+bh_status bh_ctx_destroy(bh_ctx* ctx);
+/* Pre-allocate workspaces for MSMs up to max_msm_len and domains up to 2^max_log_domain,
+ * so that later calls allocate nothing. */
+bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domain);
+/* Force a window size for device MSMs (0 = automatic). Results never depend on it. */
+bh_status bh_ctx_set_window(bh_ctx* ctx, int c);
+
+/* ---- bases (Source over Arc<Vec<G1Affine|G2Affine>>) */
+bh_status bh_srs_upload(bh_ctx* ctx, int group, const uint8_t* uncompressed_be, size_t n, int checked,
+                        bh_srs** out);
+bh_status bh_srs_free(bh_srs* srs);
+size_t bh_srs_len(const bh_srs* srs);
+/* read back base i as uncompressed bytes (96/192 B) */
+bh_status bh_srs_get(const bh_srs* srs, size_t i, uint8_t* out);
+
+/* ---- multiexp::multiexp.  density_words == NULL means FullDensity.  out: uncompressed
+ * encoding of the projective result normalised to affine (96 B for G1, 192 B for G2). */
+bh_status bh_multiexp(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint64_t* density_words,
+                      size_t density_len, const uint64_t* exponents, size_t n, int scalar_format, uint8_t* out);
+
+/* ---- EvaluationDomain.  Arrays hold 2^log_m Montgomery Fr (4 u64 each), in place. */
+bh_status bh_domain_size(size_t len, size_t* m, uint32_t* log_m);
+bh_status bh_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
+bh_status bh_ifft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
+bh_status bh_coset_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
+bh_status bh_icoset_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
+bh_status bh_distribute_powers(bh_ctx* ctx, uint64_t* coeffs, size_t len, const uint64_t g_mont[4]);
+bh_status bh_divide_by_z_on_coset(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
+bh_status bh_mul_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len);
+bh_status bh_sub_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len);
+/* H block of create_proof: a, b, c hold num_constraints evaluations each (padded to m
+ * internally); h_out receives m-1 Montgomery coefficients; *h_len = m-1. */
+bh_status bh_compute_h(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                       size_t num_constraints, uint64_t* h_out, size_t* h_len);
+
+/* ---- Parameters (groth16/mod.rs:224-477) */
+/* Parameters::read format (VerifyingKey::write then u32-BE length-prefixed h, l, a, b_g1, b_g2). */
+bh_status bh_params_load(bh_ctx* ctx, const uint8_t* bytes, size_t len, int checked, bh_params** out);
+bh_status bh_params_free(bh_params* p);
+/* sizes: [h, l, a, b_g1, b_g2, ic] */
+bh_status bh_params_sizes(const bh_params* p, size_t out[6]);
+
+/* ---- prover (create_proof after synthesis, prover.rs:206-349) */
+/* a,b,c: num_constraints Montgomery Fr (ProvingAssignment a/b/c incl. the input constraints);
+ * assignments Montgomery; densities: bit words (a_aux: num_aux bits, b_input: num_inputs bits,
+ * b_aux: num_aux bits); r, s canonical (4 LE u64).  proof_out: Proof::write, 192 B. */
+bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                   size_t num_constraints, const uint64_t* input_assignment, size_t num_inputs,
+                   const uint64_t* aux_assignment, size_t num_aux, const uint64_t* a_aux_density,
+                   const uint64_t* b_input_density, const uint64_t* b_aux_density, const uint64_t r[4],
+                   const uint64_t s[4], uint8_t proof_out[192]);
+/* Same, split into an upload (witness becomes device-resident) and the proof proper. */
+bh_status bh_witness_upload(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                            size_t num_constraints, const uint64_t* input_assignment, size_t num_inputs,
+                            const uint64_t* aux_assignment, size_t num_aux, const uint64_t* a_aux_density,
+                            const uint64_t* b_input_density, const uint64_t* b_aux_density, bh_witness** out);
+bh_status bh_witness_free(bh_witness* w);
+bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r[4],
+                           const uint64_t s[4], uint8_t proof_out[192]);
+
+/* ---- synthetic workload: MiMC chain (mimc_mod.rs:40-130 with R rounds, seeded constants),
+ * synthesized natively (witness) and its CRS generated on the device with the classic
+ * algorithm (generator.rs:310-572) from the given toxic waste (canonical u64 each). */
+bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness** out);
+bh_status bh_chain_params(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t alpha, uint64_t beta, uint64_t gamma,
+                          uint64_t delta, uint64_t tau, bh_params** out);
+/* Parameters::write of device-resident params (for parity tests; host copy). */
+bh_status bh_params_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written);
+
+/* ---- timing of the last bh_prove_witness (device events on the prover stream), ms */
+bh_status bh_last_timings(const bh_ctx* ctx, double out[8]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BELLMAN_HIP_H */

@@ -1,0 +1,240 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle's committed
+golden vectors and live oracle runs on the same seeded inputs.  Bit-exact for
+every integer/group result."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _bh():
+    import bellman_hip as bh
+    return bh
+
+
+def _bases(ctx, group, hexes):
+    bh = _bh()
+    return bh.Bases(ctx, group, b"".join(bytes.fromhex(h) for h in hexes))
+
+
+def _run_cases(ctx, group, data):
+    bh = _bh()
+    bases = _bases(ctx, group, data["bases"])
+    assert len(bases) == len(data["bases"])
+    for case in data["cases"]:
+        exps = [int(x, 16) for x in case["exps"]]
+        dens = None if case["density"] is None else [c == "1" for c in case["density"]]
+        for mont in (False, True):
+            try:
+                got = bh.multiexp(ctx, bases, case["offset"], dens, exps, montgomery=mont)
+                assert "point" in case, f"{case['note']}: expected error {case.get('error')}"
+                assert got.hex() == case["point"], case["note"]
+            except bh.SynthesisError as e:
+                assert case.get("error") == e.code, (case["note"], e)
+
+
+def test_srs_roundtrip(ctx, golden):
+    bh = _bh()
+    b = _bases(ctx, bh.BH_G1, golden["msm_g1"]["bases"][:8])
+    for i in range(8):
+        assert b.get(i).hex() == golden["msm_g1"]["bases"][i]
+    b2 = _bases(ctx, bh.BH_G2, golden["msm_g2"]["bases"][:4])
+    for i in range(4):
+        assert b2.get(i).hex() == golden["msm_g2"]["bases"][i]
+
+
+def test_srs_rejects_bad_points(ctx, golden):
+    bh = _bh()
+    raw = bytearray(bytes.fromhex(golden["msm_g1"]["bases"][0]))
+    raw[-1] ^= 1  # off the curve
+    with pytest.raises(bh.SynthesisError) as e:
+        bh.Bases(ctx, bh.BH_G1, bytes(raw), checked=True)
+    assert e.value.code == 12
+    bh.Bases(ctx, bh.BH_G1, bytes(raw), checked=False)  # unchecked read accepts it
+    big = bytearray(96)
+    big[0] = 0x1F
+    big[1:48] = b"\xff" * 47  # x >= p
+    with pytest.raises(bh.SynthesisError):
+        bh.Bases(ctx, bh.BH_G1, bytes(big), checked=False)
+
+
+def test_msm_g1_golden(ctx, golden):
+    _run_cases(ctx, _bh().BH_G1, golden["msm_g1"])
+
+
+def test_msm_g2_golden(ctx, golden):
+    _run_cases(ctx, _bh().BH_G2, golden["msm_g2"])
+
+
+@pytest.mark.parametrize("c", [4, 7, 11, 16])
+def test_msm_window_independent(ctx, golden, c):
+    """Device window size never changes the result (forced c)."""
+    bh = _bh()
+    data = golden["msm_g1"]
+    bases = _bases(ctx, bh.BH_G1, data["bases"])
+    case = [k for k in data["cases"] if k["note"].startswith("random n=160")][0]
+    exps = [int(x, 16) for x in case["exps"]]
+    ctx.set_window(c)
+    try:
+        assert bh.multiexp(ctx, bases, 0, None, exps).hex() == case["point"]
+    finally:
+        ctx.set_window(0)
+
+
+def test_msm_identity_base_semantics(ctx, golden):
+    """Source::next rejects an identity base (multiexp.rs:63-65) only when consumed
+    with a non-zero exponent; compare with the oracle restatement."""
+    bh = _bh()
+    from oracle import bellman as bm
+    from oracle import bls12_381 as bls
+    hexes = list(golden["msm_g1"]["bases"][:40])
+    ident = "40" + "00" * 95
+    hexes[5] = ident
+    bases = _bases(ctx, bh.BH_G1, hexes)
+    pts = []
+    for h in hexes:
+        ok, p = bls.g1_from_uncompressed(bytes.fromhex(h), checked=False)
+        pts.append(p)
+    rng = random.Random(9)
+    E = bm.BLS12_381
+    for exps in ([rng.randrange(R) for _ in range(40)],
+                 [0 if i == 5 else rng.randrange(R) for i in range(40)],
+                 [1 if i == 5 else rng.randrange(R) for i in range(40)]):
+        try:
+            want = ("point", bls.g1_to_uncompressed(E.G1.to_affine(bm.multiexp(E, E.G1, pts, 0, None, exps))).hex())
+        except bm.SynthesisError as e:
+            want = ("error", e.code)
+        try:
+            got = ("point", bh.multiexp(ctx, bases, 0, None, exps).hex())
+        except bh.SynthesisError as e:
+            got = ("error", e.code)
+        assert got == want
+
+
+def test_msm_density_mismatch(ctx, golden):
+    bh = _bh()
+    bases = _bases(ctx, bh.BH_G1, golden["msm_g1"]["bases"][:10])
+    with pytest.raises(bh.DensitySizeMismatch):
+        bh.multiexp(ctx, bases, 0, [True] * 5, [1] * 10)
+
+
+def test_msm_medium_vs_oracle_naive(ctx):
+    """n = 2^12 random bases / scalars (dense 255-bit) vs the oracle's naive sum."""
+    bh = _bh()
+    from oracle import bls12_381 as bls
+    rng = random.Random(12)
+    G = bls.G1
+    n = 4096
+    # bases P_i = [k_i] G built incrementally to keep the oracle fast
+    step = G.mul(G.generator(), rng.randrange(1, R))
+    acc = G.mul(G.generator(), rng.randrange(1, R))
+    pts, enc = [], []
+    for i in range(n):
+        acc = G.add(acc, step)
+        a = G.to_affine(acc)
+        pts.append(a)
+        enc.append(bls.g1_to_uncompressed(a))
+    bases = bh.Bases(ctx, bh.BH_G1, b"".join(enc))
+    exps = [rng.randrange(R) for _ in range(n)]
+    got = bh.multiexp(ctx, bases, 0, None, exps)
+    # exact oracle value by linearity: P_i = B + (i+1) S with B = acc - n*S
+    B = G.add(acc, G.neg(G.mul(step, n)))
+    se = sum(exps) % R
+    sie = sum((i + 1) * e for i, e in enumerate(exps)) % R
+    want = G.to_affine(G.add(G.mul(B, se), G.mul(step, sie)))
+    assert got.hex() == bls.g1_to_uncompressed(want).hex()
+
+
+def test_domain_ops_golden(ctx, golden):
+    bh = _bh()
+    for case in golden["domain"]:
+        coeffs = [int(x, 16) for x in case["coeffs"]]
+        other = [int(x, 16) for x in case["other"]]
+        for op, want in case["results"].items():
+            d = bh.EvaluationDomain(ctx, coeffs)
+            if op == "distribute_powers_12345":
+                d.distribute_powers(12345)
+            elif op in ("mul_assign", "sub_assign"):
+                getattr(d, op)(bh.EvaluationDomain(ctx, other))
+            else:
+                getattr(d, op)()
+            assert [format(v, "x") for v in d.into_coeffs()] == want, (case["log_m"], op)
+
+
+@pytest.mark.parametrize("logm", [10, 12, 14])
+def test_fft_roundtrip_and_linearity(ctx, logm):
+    """Size-independent properties at larger sizes: ifft(fft(x)) = x, icoset(coset(x)) = x,
+    fft linear, and fft of a delta is all-ones."""
+    bh = _bh()
+    rng = np.random.default_rng(logm)
+    m = 1 << logm
+    vals = [int(x) for x in rng.integers(0, 2**62, size=m)]
+    d = bh.EvaluationDomain(ctx, vals)
+    orig = d.coeffs.copy()
+    d.fft(); d.ifft()
+    assert np.array_equal(d.coeffs, orig)
+    d.coset_fft(); d.icoset_fft()
+    assert np.array_equal(d.coeffs, orig)
+    delta = bh.EvaluationDomain(ctx, [1] + [0] * (m - 1))
+    delta.fft()
+    assert delta.into_coeffs() == [1] * m
+
+
+def test_compute_h_golden(ctx, golden):
+    bh = _bh()
+    g = golden["h_random"]
+    a, b, c = ([int(x, 16) for x in g[k]] for k in "abc")
+    assert [format(v, "x") for v in bh.compute_h(ctx, a, b, c)] == g["h"]
+
+
+def _proof_from_fixture(ctx, fx):
+    bh = _bh()
+    params = bh.Parameters.read(ctx, bytes.fromhex(fx["params"]))
+
+    class P:  # a completed ProvingAssignment
+        pass
+    p = P()
+    p.a, p.b, p.c = ([int(x, 16) for x in fx[k]] for k in "abc")
+    p.input_assignment = [int(x, 16) for x in fx["inputs"]]
+    p.aux_assignment = [int(x, 16) for x in fx["aux"]]
+    for k in ("a_aux_density", "b_input_density", "b_aux_density"):
+        t = bh.DensityTracker()
+        t.bv = [ch == "1" for ch in fx[k]]
+        setattr(p, k, t)
+    w = bh.Witness.from_assignment(ctx, p)
+    return params, w
+
+
+def test_proofs_golden(ctx, golden):
+    bh = _bh()
+    for fx in golden["proofs"]:
+        params, w = _proof_from_fixture(ctx, fx)
+        proof = bh.prove_witness(ctx, params, w, fx["r"], fx["s"])
+        assert proof.hex() == fx["proof"], fx["name"]
+        assert params.write().hex() == fx["params"], fx["name"]
+
+
+def test_create_proof_host_synthesis(ctx, golden):
+    """create_random_proof through the product's own host synthesis (prover.rs:158-204)."""
+    bh = _bh()
+    from oracle import circuits as cc
+    fx = [f for f in golden["proofs"] if f["name"] == "mimc_chain_r15"][0]
+    params = bh.Parameters.read(ctx, bytes.fromhex(fx["params"]))
+    proof = bh.create_random_proof(ctx, cc.chain_circuit(R, 15), params)
+    assert proof.hex() == fx["proof"]
+
+
+@pytest.mark.parametrize("name,rounds", [("mimc_chain_r7", 7), ("mimc_chain_r15", 15)])
+def test_native_chain_params_and_witness(ctx, golden, name, rounds):
+    """Native C++ synthesis + device CRS generation reproduce the oracle's
+    Parameters bytes and proof bytes exactly."""
+    bh = _bh()
+    fx = [f for f in golden["proofs"] if f["name"] == name][0]
+    params = bh.Parameters.chain(ctx, rounds)
+    assert params.write().hex() == fx["params"]
+    w = bh.Witness.chain(ctx, rounds)
+    assert bh.prove_witness(ctx, params, w, 27134, 17146).hex() == fx["proof"]
