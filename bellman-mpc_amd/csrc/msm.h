@@ -23,7 +23,8 @@ struct MsmTiming {
 template <class C>
 struct MsmWorkspace {
   size_t cap_n = 0, cap_E = 0, cap_nbt = 0, cap_segs = 0, cap_T = 0;
-  uint32_t *entries = nullptr, *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *scan_scratch = nullptr;
+  uint32_t *entries = nullptr, *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *scan_scratch = nullptr,
+           *cont_bucket = nullptr;
   typename C::P *bucket_sums = nullptr, *conts = nullptr, *seg_weighted = nullptr, *seg_sum = nullptr,
                 *window_sums = nullptr;
   typename C::P* host_window_sums = nullptr;  // pinned, W entries after the stream completes

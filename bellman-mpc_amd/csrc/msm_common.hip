@@ -204,24 +204,36 @@ __global__ void __launch_bounds__(256) k_scatter(const uint32_t* scalars, size_t
   }
 }
 
+// Window choice: c ~ log2(n) - 6, clamped to [4, 16], preferring the c in
+// {c-1, c, c+1} whose top window is fullest (a nearly empty top window piles
+// every scalar into a handful of giant buckets).  Segment length S keeps about
+// 2^18 accumulation threads in flight.  Results never depend on either choice.
 MsmShape msm_shape(size_t n, int c_override) {
   MsmShape sh;
   int c = c_override;
   if (c <= 0) {
     int lg = 0;
     while (((size_t)1 << (lg + 1)) <= n) lg++;
-    c = lg - 6;
-    if (c < 4) c = 4;
-    if (c > 16) c = 16;
+    int c0 = std::max(4, std::min(16, lg - 6));
+    int best = c0, best_fill = -1;
+    for (int cc = std::max(4, c0 - 1); cc <= std::min(16, c0 + 1); cc++) {
+      const int W = (256 + cc - 1) / cc;
+      const int top = 256 - (W - 1) * cc;  // bits in the top window
+      const int fill = top * 16 / cc;      // 0..16
+      if (fill > best_fill || (fill == best_fill && cc == c0)) { best = cc; best_fill = fill; }
+    }
+    c = best;
   }
   sh.c = c;
   sh.W = (256 + c - 1) / c;
   sh.NB = 1 << (c - 1);
   sh.L = std::min<int>(8, sh.NB);
-  sh.S = 64;
+  size_t E = n * (size_t)sh.W;
+  int S = 16;
+  while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;
+  sh.S = S;
   return sh;
 }
-
 
 hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, const MsmShape& sh,
                        uint32_t* counts, hipStream_t st) {

@@ -58,7 +58,8 @@ __device__ __forceinline__ uint32_t find_bucket(const uint32_t* offsets, uint32_
   return lo;
 }
 
-// full sum of bucket gb (0..nbt): own partial + continuation partials
+// full sum of bucket gb: own partial + the (tree-reduced) continuation partials,
+// which k_cont_tree has folded into conts[s_first + 1]
 template <class C>
 __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_t* counts, const uint32_t* offsets,
                                                       const typename C::P* bucket_sums, const typename C::P* conts,
@@ -68,8 +69,29 @@ __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_
   typename C::P v = load_point<C>(&bucket_sums[gb]);
   const uint32_t off = offsets[gb];
   const uint32_t s_first = off / S, s_last = (off + cnt - 1) / S;
-  for (uint32_t s = s_first + 1; s <= s_last; s++) v = C::add(v, load_point<C>(&conts[s]));
+  if (s_last > s_first) v = C::add(v, load_point<C>(&conts[s_first + 1]));
   return v;
+}
+
+// Level k of a segmented tree reduction over the continuation partials of each
+// bucket (a bucket spanning segments s_first..s_last owns conts[s_first+1..s_last]).
+// After levels 0..K-1, conts[s_first+1] holds their sum.
+template <class C>
+__global__ void __launch_bounds__(256) k_cont_tree(const uint32_t* cont_bucket, const uint32_t* counts,
+                                                   const uint32_t* offsets, uint32_t nbt, uint32_t S, int level,
+                                                   typename C::P* conts) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t E = offsets[nbt];
+  if ((size_t)s * S >= E) return;
+  const uint32_t b = cont_bucket[s];
+  if (b == 0xffffffffu) return;
+  const uint32_t off = offsets[b];
+  const uint32_t s_first = off / S;
+  const uint32_t ncont = (off + counts[b] - 1) / S - s_first;
+  const uint32_t j = s - s_first - 1;
+  const uint32_t half = 1u << level;
+  if ((j & ((half << 1) - 1)) != 0 || j + half >= ncont) return;
+  store_point<C>(&conts[s], C::add(load_point<C>(&conts[s]), load_point<C>(&conts[s + half])));
 }
 
 // thread (w, t): buckets [t*L, (t+1)*L) of window w
@@ -132,7 +154,8 @@ __global__ void __launch_bounds__(BLOCK) k_tree_reduce(const typename C::P* pts,
 template <class C>
 __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                                                         const uint32_t* bases, uint32_t S,
-                                                        typename C::P* bucket_sums, typename C::P* conts) {
+                                                        typename C::P* bucket_sums, typename C::P* conts,
+                                                        uint32_t* cont_bucket) {
   const uint32_t E = offsets[nbt];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t pos0 = seg * S;
@@ -141,6 +164,7 @@ __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries,
   uint32_t b = find_bucket(offsets, nbt, pos0);
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
+  cont_bucket[seg] = started_here ? 0xffffffffu : b;
   typename C::P acc = C::identity();
   for (uint32_t j = pos0; j < end; j++) {
     if (j == next) {
@@ -196,8 +220,11 @@ hipError_t MsmWorkspace<C>::grow(size_t E, size_t nbt, size_t segs, size_t T) {
   }
   if (segs > cap_segs) {
     if (conts) hipFree(conts);
+    if (cont_bucket) hipFree(cont_bucket);
     conts = nullptr;
+    cont_bucket = nullptr;
     if ((err = hipMalloc(&conts, segs * sizeof(typename C::P))) != hipSuccess) return err;
+    if ((err = hipMalloc(&cont_bucket, segs * 4)) != hipSuccess) return err;
     cap_segs = segs;
   }
   if (T > cap_T) {
@@ -247,6 +274,8 @@ void MsmWorkspace<C>::release() {
   if (scan_scratch) hipFree(scan_scratch);
   if (bucket_sums) hipFree(bucket_sums);
   if (conts) hipFree(conts);
+  if (cont_bucket) hipFree(cont_bucket);
+  cont_bucket = nullptr;
   if (seg_weighted) hipFree(seg_weighted);
   if (seg_sum) hipFree(seg_sum);
   if (window_sums) hipFree(window_sums);
@@ -276,8 +305,12 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
     const size_t segs = (Emax + sh.S - 1) / sh.S;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries, ws.offsets,
-                       (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts);
+                       (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
+    // log-depth reduction of continuation partials (a bucket can span up to segs segments)
+    for (int level = 0; ((size_t)1 << level) < segs; level++)
+      hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
+                         ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   }
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
   const size_t total = (size_t)sh.W * T;

@@ -58,10 +58,25 @@ void write_vec(const bh_srs& v, std::vector<uint8_t>& out) {
   const size_t n = v.n;
   out.push_back((uint8_t)(n >> 24)); out.push_back((uint8_t)(n >> 16));
   out.push_back((uint8_t)(n >> 8)); out.push_back((uint8_t)n);
-  uint8_t buf[192];
+  if (!n) return;
+  const int words = v.group == BH_G1 ? 24 : 48;
+  std::vector<uint32_t> w(n * words);
+  (void)hipMemcpy(w.data(), v.pts.p, n * words * 4, hipMemcpyDeviceToHost);
+  std::vector<char> inf(n, 0);
+  for (size_t k : v.identity_idx) inf[k] = 1;
+  const size_t pb = v.group == BH_G1 ? 96 : 192;
+  const size_t base = out.size();
+  out.resize(base + n * pb);
   for (size_t i = 0; i < n; i++) {
-    bh_srs_get(&v, i, buf);
-    out.insert(out.end(), buf, buf + (v.group == BH_G1 ? 96 : 192));
+    const uint32_t* d = &w[i * words];
+    uint8_t* o = &out[base + i * pb];
+    if (v.group == BH_G1) {
+      g1_to_uncompressed(AffinePt<Fp>{fp_from_dev_words(d), fp_from_dev_words(d + 12), inf[i] != 0}, o);
+    } else {
+      g2_to_uncompressed(AffinePt<bh::Fp2>{bh::Fp2{fp_from_dev_words(d), fp_from_dev_words(d + 12)},
+                                           bh::Fp2{fp_from_dev_words(d + 24), fp_from_dev_words(d + 36)}, inf[i] != 0},
+                         o);
+    }
   }
 }
 

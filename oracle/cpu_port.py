@@ -1,0 +1,50 @@
+"""ORACLE / CPU BASELINE wrapper (test + bench infrastructure only).
+
+ctypes binding of oracle/cpu/libbellman_port.so, the C++ restatement of
+bellman's multicore prover core (see oracle/cpu/bellman_port.cpp header).
+Used by tests/ (as a checker) and by bench.py's cpu_baseline leg."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "cpu", "libbellman_port.so")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "cpu")], check=True)
+
+
+def _lib():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    P, S, U64, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+    lib.bp_chain_prove.restype = I
+    lib.bp_chain_prove.argtypes = [P, S, S, U64, I, I, P, P, P, P, P]
+    lib.bp_hardware_threads.restype = I
+    return lib
+
+
+def hardware_threads():
+    return _lib().bp_hardware_threads()
+
+
+def chain_prove(params_bytes, rounds, seed=7, threads=0, reps=1, r=27134, s=17146):
+    """Synthesize the MiMC chain and run the bellman-algorithm prover core.
+    Returns (proof bytes, median core ms, synthesis ms)."""
+    lib = _lib()
+    buf = np.frombuffer(params_bytes, dtype=np.uint8)
+    rr = np.array([r, 0, 0, 0], dtype=np.uint64)
+    ss = np.array([s, 0, 0, 0], dtype=np.uint64)
+    out = np.zeros(192, dtype=np.uint8)
+    ms = ctypes.c_double()
+    ms_syn = ctypes.c_double()
+    st = lib.bp_chain_prove(buf.ctypes.data_as(ctypes.c_void_p), len(params_bytes), rounds, seed, threads, reps,
+                            rr.ctypes.data_as(ctypes.c_void_p), ss.ctypes.data_as(ctypes.c_void_p),
+                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ms), ctypes.byref(ms_syn))
+    if st != 0:
+        raise RuntimeError(f"bellman port failed with status {st}")
+    return out.tobytes(), ms.value, ms_syn.value
