@@ -102,6 +102,16 @@ def _load():
         "bh_chain_witness": (I, [P, S, U64, P]),
         "bh_chain_params": (I, [P, S, U64, U64, U64, U64, U64, U64, P]),
         "bh_last_timings": (I, [P, P]),
+        "bh_shard_range": (I, [S, S, S, P, P]),
+        "bh_prove_witness_partial": (I, [P, P, P, S, S, P]),
+        "bh_vk_write": (I, [P, P, S, P]),
+        "bh_proof_from_partials": (I, [P, S, P, S, P, P, P]),
+        "bh_comm_unique_id": (I, [P]),
+        "bh_comm_init": (I, [P, P, I, I, P]),
+        "bh_comm_allgather_partials": (I, [P, P, P]),
+        "bh_comm_destroy": (I, [P]),
+        "bh_ctx_synchronize": (I, [P]),
+        "bh_device_count": (I, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -119,8 +129,11 @@ EXPORTED_SYMBOLS = [
     "bh_ifft", "bh_coset_fft", "bh_icoset_fft", "bh_distribute_powers", "bh_divide_by_z_on_coset",
     "bh_mul_assign", "bh_sub_assign", "bh_compute_h", "bh_params_load", "bh_params_free", "bh_params_sizes",
     "bh_prove", "bh_witness_upload", "bh_witness_free", "bh_prove_witness", "bh_chain_witness",
-    "bh_chain_params", "bh_params_write", "bh_last_timings",
+    "bh_chain_params", "bh_params_write", "bh_last_timings", "bh_shard_range", "bh_prove_witness_partial",
+    "bh_vk_write", "bh_proof_from_partials", "bh_comm_unique_id", "bh_comm_init", "bh_comm_allgather_partials",
+    "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count",
 ]
+PARTIAL_BYTES = 960
 
 
 def lib():
@@ -192,6 +205,9 @@ class Context:
 
     def set_window(self, c):
         _check(_lib.bh_ctx_set_window(self.h, c), "bh_ctx_set_window")
+
+    def synchronize(self):
+        _check(_lib.bh_ctx_synchronize(self.h))
 
     def last_timings(self):
         out = (ctypes.c_double * 8)()
@@ -358,6 +374,14 @@ class Parameters:
         _check(_lib.bh_params_write(self.h, None, 0, ctypes.byref(n)))
         out = np.zeros(n.value, dtype=np.uint8)
         _check(_lib.bh_params_write(self.h, _ptr(out), n.value, ctypes.byref(n)))
+        return out.tobytes()
+
+    def vk_bytes(self):
+        """VerifyingKey::write (groth16/mod.rs:146-159)."""
+        n = ctypes.c_size_t()
+        _check(_lib.bh_vk_write(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, dtype=np.uint8)
+        _check(_lib.bh_vk_write(self.h, _ptr(out), n.value, ctypes.byref(n)))
         return out.tobytes()
 
     def __del__(self):
@@ -536,3 +560,60 @@ def create_proof(ctx, circuit, params, r, s):
 def create_random_proof(ctx, circuit, params, rng=None):
     """prover.rs:158-173: the fork ignores rng and uses r = 27134, s = 17146."""
     return create_proof(ctx, circuit, params, 27134, 17146)
+
+
+# ------------------------------------------------------------------ multi-GPU (MSM sharding)
+def shard_range(n, shard, nshards):
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(_lib.bh_shard_range(n, shard, nshards, ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
+def prove_witness_partial(ctx, params, witness, shard, nshards):
+    """This rank's partial sums of the 8 multiexps (960 bytes)."""
+    out = np.zeros(PARTIAL_BYTES, dtype=np.uint8)
+    _check(_lib.bh_prove_witness_partial(ctx.h, params.h, witness.h, shard, nshards, _ptr(out)), "partial")
+    return out.tobytes()
+
+
+def proof_from_partials(vk_bytes, partials, nshards, r, s):
+    """Host-only: sum the gathered partials (shard order) and assemble the proof."""
+    vk = np.frombuffer(vk_bytes, dtype=np.uint8)
+    parts = np.frombuffer(partials, dtype=np.uint8)
+    assert parts.size == nshards * PARTIAL_BYTES
+    out = np.zeros(192, dtype=np.uint8)
+    rr, ss = fr_to_canonical_limbs([r])[0], fr_to_canonical_limbs([s])[0]
+    _check(_lib.bh_proof_from_partials(_ptr(vk), vk.size, _ptr(parts), nshards, _ptr(rr), _ptr(ss), _ptr(out)),
+           "proof_from_partials")
+    return out.tobytes()
+
+
+def device_count():
+    return _lib.bh_device_count()
+
+
+class Comm:
+    """RCCL communicator for the partial-sum exchange (bh_comm_*)."""
+
+    @staticmethod
+    def unique_id():
+        out = np.zeros(128, dtype=np.uint8)
+        _check(_lib.bh_comm_unique_id(_ptr(out)), "ncclGetUniqueId")
+        return out.tobytes()
+
+    def __init__(self, ctx, uid, nranks, rank):
+        b = np.frombuffer(uid, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_comm_init(ctx.h, _ptr(b), nranks, rank, ctypes.byref(h)), "ncclCommInitRank")
+        self.h, self.nranks = h, nranks
+
+    def allgather(self, partial):
+        src = np.frombuffer(partial, dtype=np.uint8)
+        out = np.zeros(self.nranks * PARTIAL_BYTES, dtype=np.uint8)
+        _check(_lib.bh_comm_allgather_partials(self.h, _ptr(src), _ptr(out)), "ncclAllGather")
+        return out.tobytes()
+
+    def close(self):
+        if self.h:
+            _lib.bh_comm_destroy(self.h)
+            self.h = None

@@ -1,0 +1,87 @@
+// Multi-GPU exchange step over RCCL (xGMI): the all-gather of the per-rank
+// partial multiexp records (BH_PARTIAL_BYTES each).  Elliptic-curve addition is
+// not an RCCL reduction operator, so the "reduce" is an all-gather of the
+// affine partial sums followed by the host-side sum in bh_proof_from_partials.
+// The reference has no multi-device path; this is the MI355X
+// replacement for its single-process rayon fan-out (prover.rs:233-307).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <string.h>
+
+#include "api_internal.h"
+
+struct bh_comm {
+  bh_ctx* ctx = nullptr;
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+  uint8_t* d_send = nullptr;
+  uint8_t* d_recv = nullptr;
+};
+
+extern "C" {
+
+bh_status bh_comm_unique_id(uint8_t out[128]) {
+  if (!out) return BH_ERR_INVALID_ARGUMENT;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return BH_ERR_HIP;
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(out, &id, sizeof id);
+  return BH_OK;
+}
+
+bh_status bh_comm_init(bh_ctx* ctx, const uint8_t id[128], int nranks, int rank, bh_comm** out) {
+  if (!ctx || !id || !out || nranks <= 0 || rank < 0 || rank >= nranks) return BH_ERR_INVALID_ARGUMENT;
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  bh_comm* c = new bh_comm();
+  c->ctx = ctx;
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  if (ncclCommInitRank(&c->comm, nranks, uid, rank) != ncclSuccess) { delete c; return BH_ERR_HIP; }
+  if (hipMalloc(&c->d_send, BH_PARTIAL_BYTES) != hipSuccess ||
+      hipMalloc(&c->d_recv, (size_t)BH_PARTIAL_BYTES * nranks) != hipSuccess) {
+    ncclCommDestroy(c->comm);
+    delete c;
+    return BH_ERR_OUT_OF_MEMORY;
+  }
+  *out = c;
+  return BH_OK;
+}
+
+bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t* all_out) {
+  if (!c || !partial || !all_out) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(c->ctx->mu);
+  BH_TRY_HIP(hipSetDevice(c->ctx->device));
+  hipStream_t st = c->ctx->stream;
+  BH_TRY_HIP(hipMemcpyAsync(c->d_send, partial, BH_PARTIAL_BYTES, hipMemcpyHostToDevice, st));
+  if (ncclAllGather(c->d_send, c->d_recv, BH_PARTIAL_BYTES, ncclUint8, c->comm, st) != ncclSuccess) return BH_ERR_HIP;
+  BH_TRY_HIP(hipMemcpyAsync(all_out, c->d_recv, (size_t)BH_PARTIAL_BYTES * c->nranks, hipMemcpyDeviceToHost, st));
+  BH_TRY_HIP(hipStreamSynchronize(st));
+  return BH_OK;
+}
+
+bh_status bh_comm_destroy(bh_comm* c) {
+  if (!c) return BH_OK;
+  (void)hipSetDevice(c->ctx->device);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->d_send) (void)hipFree(c->d_send);
+  if (c->d_recv) (void)hipFree(c->d_recv);
+  delete c;
+  return BH_OK;
+}
+
+bh_status bh_ctx_synchronize(bh_ctx* ctx) {
+  if (!ctx) return BH_ERR_INVALID_ARGUMENT;
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  BH_TRY_HIP(hipDeviceSynchronize());
+  return BH_OK;
+}
+
+int bh_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+}  // extern "C"

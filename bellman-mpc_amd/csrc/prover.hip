@@ -217,11 +217,26 @@ bh_status bh_witness_free(bh_witness* w) {
   return BH_OK;
 }
 
-bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r_in[4],
-                           const uint64_t s_in[4], uint8_t proof_out[192]) {
-  if (!ctx || !params || !w || !r_in || !s_in || !proof_out) return BH_ERR_INVALID_ARGUMENT;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  BH_TRY_HIP(hipSetDevice(ctx->device));
+}  // extern "C"
+
+namespace {
+
+struct VkHost {
+  AffinePt<Fp> alpha_g1, beta_g1, delta_g1;
+  AffinePt<bh::Fp2> beta_g2, delta_g2;
+};
+
+// shard k of n items: [k*n/N, (k+1)*n/N)
+inline void shard_range(size_t n, size_t k, size_t N, size_t* lo, size_t* hi) {
+  *lo = (size_t)((unsigned __int128)n * k / N);
+  *hi = (size_t)((unsigned __int128)n * (k + 1) / N);
+}
+
+// The 8 multiexps of create_proof (prover.rs:233-307) restricted to scalar shard
+// `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
+// res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
+bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
+                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2]) {
   const auto t0 = std::chrono::steady_clock::now();
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
   const int L = w->log_m;
@@ -271,74 +286,44 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0;
   int g1_launches = 0, g2_launches = 0;
-  auto cnt = [](size_t n, int& launches, size_t& pairs, size_t used) { if (n) { launches++; pairs += used; } };
-
-  Jac<Fp> h, l, a_in, a_aux, b1_in, b1_aux;
-  Jac<bh::Fp2> b2_in, b2_aux;
   const uint32_t* inputs = w->inputs.as<uint32_t>();
   const uint32_t* aux = w->aux.as<uint32_t>();
   int32_t* idx = ctx->idx.as<int32_t>();
+  size_t lo, hi;
+  // one sharded G1 multiexp: scalars [lo,hi) of an n-vector; idx (if any) maps the full vector
+  auto g1 = [&](const bh_srs* srs, size_t base_off, const uint32_t* sc, size_t n, const int32_t* ix, size_t used,
+                Jac<Fp>* out) -> bh_status {
+    shard_range(n, shard, nshards, &lo, &hi);
+    bh_status st = msm_g1_device(ctx, srs, base_off + lo, sc + lo * 8, hi - lo, ix ? ix + lo : nullptr, out,
+                                 &g1_acc_ms);
+    if (hi > lo) { g1_launches++; g1_pairs += (size_t)((unsigned __int128)used * (hi - lo) / std::max<size_t>(n, 1)); }
+    return st;
+  };
+  auto g2 = [&](const bh_srs* srs, size_t base_off, const uint32_t* sc, size_t n, const int32_t* ix, size_t used,
+                Jac<bh::Fp2>* out) -> bh_status {
+    shard_range(n, shard, nshards, &lo, &hi);
+    bh_status st = msm_g2_device(ctx, srs, base_off + lo, sc + lo * 8, hi - lo, ix ? ix + lo : nullptr, out,
+                                 &g2_acc_ms);
+    if (hi > lo) { g2_launches++; g2_pairs += (size_t)((unsigned __int128)used * (hi - lo) / std::max<size_t>(n, 1)); }
+    return st;
+  };
   // h: FullDensity over params.h (prover.rs:233)
-  if ((s = msm_g1_device(ctx, &params->h, 0, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, &h, &g1_acc_ms))) return s;
-  cnt(m - 1, g1_launches, g1_pairs, m - 1);
+  if ((s = g1(&params->h, 0, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, &res1[0]))) return s;
   // l: FullDensity over aux (prover.rs:252-257)
-  if ((s = msm_g1_device(ctx, &params->l, 0, aux, na, nullptr, &l, &g1_acc_ms))) return s;
-  cnt(na, g1_launches, g1_pairs, na);
+  if ((s = g1(&params->l, 0, aux, na, nullptr, na, &res1[1]))) return s;
   // a_inputs / a_aux (prover.rs:259-275)
-  if ((s = msm_g1_device(ctx, &params->a, 0, inputs, ni, nullptr, &a_in, &g1_acc_ms))) return s;
-  cnt(ni, g1_launches, g1_pairs, ni);
-  if (na) {
-    BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(),
-                             ctx->stream));
-  }
-  if ((s = msm_g1_device(ctx, &params->a, ni, aux, na, idx, &a_aux, &g1_acc_ms))) return s;
-  cnt(na, g1_launches, g1_pairs, w->a_aux_total);
-  // b_g1 (prover.rs:277-296)
-  if (ni) {
-    BH_TRY_HIP(density_index(d_b_in, ni, 0, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), ctx->stream));
-  }
-  if ((s = msm_g1_device(ctx, &params->b_g1, 0, inputs, ni, idx, &b1_in, &g1_acc_ms))) return s;
-  cnt(ni, g1_launches, g1_pairs, w->b_in_total);
-  if ((s = msm_g2_device(ctx, &params->b_g2, 0, inputs, ni, idx, &b2_in, &g2_acc_ms))) return s;
-  cnt(ni, g2_launches, g2_pairs, w->b_in_total);
-  if (na) {
-    BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx, ctx->dtmp.as<uint32_t>(),
-                             ctx->dscan.as<uint32_t>(), ctx->stream));
-  }
-  if ((s = msm_g1_device(ctx, &params->b_g1, w->b_in_total, aux, na, idx, &b1_aux, &g1_acc_ms))) return s;
-  cnt(na, g1_launches, g1_pairs, w->b_aux_total);
-  // b_g2 (prover.rs:298-307)
-  if ((s = msm_g2_device(ctx, &params->b_g2, w->b_in_total, aux, na, idx, &b2_aux, &g2_acc_ms))) return s;
-  cnt(na, g2_launches, g2_pairs, w->b_aux_total);
-
-  // ---- assembly (prover.rs:315-349)
-  Fr r = fr_from_canonical(r_in), sv = fr_from_canonical(s_in);
-  uint64_t rc[4], sc[4], rsc[4];
-  fr_to_canonical(r, rc);
-  fr_to_canonical(sv, sc);
-  fr_to_canonical(mul(r, sv), rsc);
-  const Jac<Fp> d1 = jac_from_affine(params->delta_g1);
-  const Jac<bh::Fp2> d2 = jac_from_affine(params->delta_g2);
-  Jac<Fp> g_a = jac_add(jac_mul(d1, rc, 4), jac_from_affine(params->alpha_g1));
-  Jac<bh::Fp2> g_b = jac_add(jac_mul(d2, sc, 4), jac_from_affine(params->beta_g2));
-  Jac<Fp> g_c = jac_mul(d1, rsc, 4);
-  g_c = jac_add(g_c, jac_mul(jac_from_affine(params->alpha_g1), sc, 4));
-  g_c = jac_add(g_c, jac_mul(jac_from_affine(params->beta_g1), rc, 4));
-  Jac<Fp> a_answer = jac_add(a_in, a_aux);
-  g_a = jac_add(g_a, a_answer);
-  a_answer = jac_mul(a_answer, sc, 4);
-  g_c = jac_add(g_c, a_answer);
-  Jac<Fp> b1_answer = jac_add(b1_in, b1_aux);
-  Jac<bh::Fp2> b2_answer = jac_add(b2_in, b2_aux);
-  g_b = jac_add(g_b, b2_answer);
-  b1_answer = jac_mul(b1_answer, rc, 4);
-  g_c = jac_add(g_c, b1_answer);
-  g_c = jac_add(g_c, h);
-  g_c = jac_add(g_c, l);
-  // Proof::write: compressed A || B || C (groth16/mod.rs:42-48)
-  g1_to_compressed(jac_to_affine(g_a), proof_out);
-  g2_to_compressed(jac_to_affine(g_b), proof_out + 48);
-  g1_to_compressed(jac_to_affine(g_c), proof_out + 144);
+  if ((s = g1(&params->a, 0, inputs, ni, nullptr, ni, &res1[2]))) return s;
+  if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(),
+                                   ctx->stream));
+  if ((s = g1(&params->a, 0, aux, na, idx, w->a_aux_total, &res1[3]))) return s;
+  // b_g1 / b_g2 inputs (prover.rs:277-307)
+  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), ctx->stream));
+  if ((s = g1(&params->b_g1, 0, inputs, ni, idx, w->b_in_total, &res1[4]))) return s;
+  if ((s = g2(&params->b_g2, 0, inputs, ni, idx, w->b_in_total, &res2[0]))) return s;
+  if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx, ctx->dtmp.as<uint32_t>(),
+                                   ctx->dscan.as<uint32_t>(), ctx->stream));
+  if ((s = g1(&params->b_g1, 0, aux, na, idx, w->b_aux_total, &res1[5]))) return s;
+  if ((s = g2(&params->b_g2, 0, aux, na, idx, w->b_aux_total, &res2[1]))) return s;
 
   const auto t1 = std::chrono::steady_clock::now();
   float h_ms = 0;
@@ -351,6 +336,138 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
   ctx->last_timings[5] = g2_acc_ms;
   ctx->last_timings[6] = g2_launches;
   ctx->last_timings[7] = (double)g2_pairs;
+  return BH_OK;
+}
+
+// proof assembly (prover.rs:315-349) -> Proof::write (groth16/mod.rs:42-48)
+void assemble(const VkHost& vk, const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], const uint64_t r_in[4],
+              const uint64_t s_in[4], uint8_t proof_out[192]) {
+  Fr r = fr_from_canonical(r_in), sv = fr_from_canonical(s_in);
+  uint64_t rc[4], sc[4], rsc[4];
+  fr_to_canonical(r, rc);
+  fr_to_canonical(sv, sc);
+  fr_to_canonical(mul(r, sv), rsc);
+  const Jac<Fp> d1 = jac_from_affine(vk.delta_g1);
+  const Jac<bh::Fp2> d2 = jac_from_affine(vk.delta_g2);
+  Jac<Fp> g_a = jac_add(jac_mul(d1, rc, 4), jac_from_affine(vk.alpha_g1));
+  Jac<bh::Fp2> g_b = jac_add(jac_mul(d2, sc, 4), jac_from_affine(vk.beta_g2));
+  Jac<Fp> g_c = jac_mul(d1, rsc, 4);
+  g_c = jac_add(g_c, jac_mul(jac_from_affine(vk.alpha_g1), sc, 4));
+  g_c = jac_add(g_c, jac_mul(jac_from_affine(vk.beta_g1), rc, 4));
+  Jac<Fp> a_answer = jac_add(r1[2], r1[3]);
+  g_a = jac_add(g_a, a_answer);
+  a_answer = jac_mul(a_answer, sc, 4);
+  g_c = jac_add(g_c, a_answer);
+  Jac<Fp> b1_answer = jac_add(r1[4], r1[5]);
+  Jac<bh::Fp2> b2_answer = jac_add(r2[0], r2[1]);
+  g_b = jac_add(g_b, b2_answer);
+  b1_answer = jac_mul(b1_answer, rc, 4);
+  g_c = jac_add(g_c, b1_answer);
+  g_c = jac_add(g_c, r1[0]);
+  g_c = jac_add(g_c, r1[1]);
+  g1_to_compressed(jac_to_affine(g_a), proof_out);
+  g2_to_compressed(jac_to_affine(g_b), proof_out + 48);
+  g1_to_compressed(jac_to_affine(g_c), proof_out + 144);
+}
+
+VkHost vk_of(const bh_params* p) {
+  return VkHost{p->alpha_g1, p->beta_g1, p->delta_g1, p->beta_g2, p->delta_g2};
+}
+
+constexpr size_t PARTIAL_BYTES = 6 * 96 + 2 * 192;
+
+}  // namespace
+
+extern "C" {
+
+bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r_in[4],
+                           const uint64_t s_in[4], uint8_t proof_out[192]) {
+  if (!ctx || !params || !w || !r_in || !s_in || !proof_out) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  bh_status s = compute_msms(ctx, params, w, 0, 1, r1, r2);
+  if (s) return s;
+  const auto t0 = std::chrono::steady_clock::now();
+  assemble(vk_of(params), r1, r2, r_in, s_in, proof_out);
+  ctx->last_timings[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BH_OK;
+}
+
+bh_status bh_shard_range(size_t n, size_t shard, size_t nshards, size_t* lo, size_t* hi) {
+  if (!lo || !hi || nshards == 0 || shard >= nshards) return BH_ERR_INVALID_ARGUMENT;
+  shard_range(n, shard, nshards, lo, hi);
+  return BH_OK;
+}
+
+bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard,
+                                   size_t nshards, uint8_t partial_out[960]) {
+  if (!ctx || !params || !w || !partial_out || nshards == 0 || shard >= nshards) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  bh_status s = compute_msms(ctx, params, w, shard, nshards, r1, r2);
+  if (s) return s;
+  for (int i = 0; i < 6; i++) g1_to_uncompressed(jac_to_affine(r1[i]), partial_out + 96 * i);
+  for (int i = 0; i < 2; i++) g2_to_uncompressed(jac_to_affine(r2[i]), partial_out + 576 + 192 * i);
+  return BH_OK;
+}
+
+bh_status bh_vk_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written) {
+  if (!p || !written) return BH_ERR_INVALID_ARGUMENT;
+  const size_t need = 96 * 3 + 192 * 3 + 4 + 96 * p->ic.size();
+  *written = need;
+  if (!out) return BH_OK;
+  if (cap < need) return BH_ERR_INVALID_ARGUMENT;
+  uint8_t* o = out;
+  g1_to_uncompressed(p->alpha_g1, o); o += 96;
+  g1_to_uncompressed(p->beta_g1, o); o += 96;
+  g2_to_uncompressed(p->beta_g2, o); o += 192;
+  g2_to_uncompressed(p->gamma_g2, o); o += 192;
+  g1_to_uncompressed(p->delta_g1, o); o += 96;
+  g2_to_uncompressed(p->delta_g2, o); o += 192;
+  const size_t n = p->ic.size();
+  o[0] = (uint8_t)(n >> 24); o[1] = (uint8_t)(n >> 16); o[2] = (uint8_t)(n >> 8); o[3] = (uint8_t)n; o += 4;
+  for (const auto& ic : p->ic) { g1_to_uncompressed(ic, o); o += 96; }
+  return BH_OK;
+}
+
+// Host-only: sum the per-shard partial multiexps (the all-gathered 960-byte records,
+// shard order) and assemble the proof.  vk: VerifyingKey::write bytes.
+bh_status bh_proof_from_partials(const uint8_t* vk_bytes, size_t vk_len, const uint8_t* partials, size_t nshards,
+                                 const uint64_t r[4], const uint64_t s[4], uint8_t proof_out[192]) {
+  if (!vk_bytes || !partials || !nshards || !r || !s || !proof_out) return BH_ERR_INVALID_ARGUMENT;
+  if (vk_len < 96 * 3 + 192 * 3) return BH_ERR_INVALID_ENCODING;
+  VkHost vk;
+  AffinePt<bh::Fp2> gamma;
+  const uint8_t* p = vk_bytes;
+  if (g1_from_uncompressed(p, &vk.alpha_g1, true)) return BH_ERR_INVALID_ENCODING;
+  if (g1_from_uncompressed(p + 96, &vk.beta_g1, true)) return BH_ERR_INVALID_ENCODING;
+  if (g2_from_uncompressed(p + 192, &vk.beta_g2, true)) return BH_ERR_INVALID_ENCODING;
+  if (g2_from_uncompressed(p + 384, &gamma, true)) return BH_ERR_INVALID_ENCODING;
+  if (g1_from_uncompressed(p + 576, &vk.delta_g1, true)) return BH_ERR_INVALID_ENCODING;
+  if (g2_from_uncompressed(p + 672, &vk.delta_g2, true)) return BH_ERR_INVALID_ENCODING;
+  if (vk.delta_g1.infinity || vk.delta_g2.infinity) return BH_ERR_UNEXPECTED_IDENTITY;  // prover.rs:309-313
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  for (int i = 0; i < 6; i++) r1[i] = jac_identity<Fp>();
+  for (int i = 0; i < 2; i++) r2[i] = jac_identity<bh::Fp2>();
+  for (size_t k = 0; k < nshards; k++) {
+    const uint8_t* q = partials + k * PARTIAL_BYTES;
+    for (int i = 0; i < 6; i++) {
+      AffinePt<Fp> a;
+      if (g1_from_uncompressed(q + 96 * i, &a, true)) return BH_ERR_INVALID_ENCODING;
+      r1[i] = jac_add(r1[i], jac_from_affine(a));
+    }
+    for (int i = 0; i < 2; i++) {
+      AffinePt<bh::Fp2> a;
+      if (g2_from_uncompressed(q + 576 + 192 * i, &a, true)) return BH_ERR_INVALID_ENCODING;
+      r2[i] = jac_add(r2[i], jac_from_affine(a));
+    }
+  }
+  assemble(vk, r1, r2, r, s, proof_out);
   return BH_OK;
 }
 

@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on a bounded sample (rank 0)")
     ap.add_argument("--cpu-log-constraints", type=int, default=16)
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
+    ap.add_argument("--exchange", default="rccl",
+                    help="partial-sum exchange: rccl (library-driven RCCL all-gather over xGMI) or gloo (CPU rehearsal)")
     return ap.parse_args()
 
 
@@ -70,17 +72,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import bellman_hip as bh
 
+    # torch.distributed is used for CPU-side rendezvous only (gloo): torch bundles its own
+    # HIP runtime, so the GPU work and the RCCL exchange are driven by libbellman_hip.
     dist = None
+    device = local % max(1, bh.device_count())  # rehearsal: several ranks may share one card
     if world > 1:
-        import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
+        dist.init_process_group("gloo")
     k = args.log_constraints
     rounds = (1 << (k - 1)) - 1
     n_constraints = 2 * rounds + 2
-    ctx = bh.Context(local)
+    ctx = bh.Context(device)
     t0 = time.time()
     params = bh.Parameters.chain(ctx, rounds)
     t_params = time.time() - t0
@@ -88,25 +90,46 @@ def main():
     witness = bh.Witness.chain(ctx, rounds)
     t_wit = time.time() - t0
     r, s = 27134, 17146
+    vk = params.vk_bytes()
+    comm = None
+    exchange = args.exchange
+    if world > 1 and exchange == "rccl":
+        obj = [bh.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        try:
+            comm = bh.Comm(ctx, obj[0], world, rank)
+        except bh.SynthesisError as e:
+            print(f"rank {rank}: RCCL communicator failed ({e}); exchanging over gloo", file=sys.stderr)
+            exchange = "gloo-fallback"
+        ok = [comm is not None]
+        allok = [None] * world
+        dist.all_gather_object(allok, ok[0])
+        if not all(allok):
+            if comm is not None:
+                comm.close()
+                comm = None
+            exchange = "gloo-fallback"
 
     def step():
         if world == 1:
             return bh.prove_witness(ctx, params, witness, r, s)
-        import torch
         part = bh.prove_witness_partial(ctx, params, witness, rank, world)
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
-        gathered = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(gathered, t)
+        if comm is not None:
+            parts = comm.allgather(part)  # ncclAllGather over xGMI
+        else:
+            import torch
+            t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
+            gathered = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(gathered, t)
+            parts = b"".join(bytes(g.numpy().tobytes()) for g in gathered)
         if rank == 0:
-            parts = b"".join(bytes(g.cpu().numpy().tobytes()) for g in gathered)
-            return bh.proof_from_partials(ctx, params, parts, world, r, s)
+            return bh.proof_from_partials(vk, parts, world, r, s)
         return None
 
     def barrier():
         if dist is not None:
-            import torch
             dist.barrier()
-            torch.cuda.synchronize()
+        ctx.synchronize()
 
     ref = None
     for _ in range(args.warmup):
@@ -125,10 +148,12 @@ def main():
     elapsed = time.perf_counter() - t_start
     if dist is not None:
         import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if rank != 0:
+        if comm is not None:
+            comm.close()
         dist.destroy_process_group()
         return
     ms = elapsed * 1000.0 / args.steps
@@ -158,7 +183,8 @@ def main():
         "dtype": "u32 limbs (BLS12-381 Fp/Fr modular integer)",
         "data": "synthetic MiMC-chain witness (splitmix64 seed 7), device-generated CRS (alpha=6,beta=24,gamma=6,delta=24,tau=2)",
         "config": {"workload": f"C3: full create_proof after synthesis, MiMC chain R={rounds}",
-                   "constraints": n_constraints, "log_domain": k, "parallelism": f"msm-shard{world}"},
+                   "constraints": n_constraints, "log_domain": k, "parallelism": f"msm-shard{world}",
+                   "exchange": exchange if world > 1 else None},
         "roofline": roof,
         "cpu_baseline": base,
         "breakdown_ms": {"h_pipeline": round(sum(t[1] for t in timings) / len(timings), 3),
@@ -169,6 +195,8 @@ def main():
         "proof_sha_prefix": ref.hex()[:32] if ref else None,
     }
     print(json.dumps(out))
+    if comm is not None:
+        comm.close()
     if dist is not None:
         dist.destroy_process_group()
 

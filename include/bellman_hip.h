@@ -130,6 +130,30 @@ bh_status bh_witness_free(bh_witness* w);
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r[4],
                            const uint64_t s[4], uint8_t proof_out[192]);
 
+/* ---- multi-GPU: every multiexp sharded by scalar range (shard k of N covers
+ * [k*n/N, (k+1)*n/N) of each query); partial_out = 8 uncompressed points
+ * [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux] (G1, 96 B) + [b_g2_inputs, b_g2_aux]
+ * (G2, 192 B) = 960 B.  The all-gathered records are summed and assembled on the
+ * host by bh_proof_from_partials (prover.rs:315-349), which needs only the
+ * VerifyingKey::write bytes (bh_vk_write). */
+#define BH_PARTIAL_BYTES 960
+bh_status bh_shard_range(size_t n, size_t shard, size_t nshards, size_t* lo, size_t* hi);
+bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard,
+                                   size_t nshards, uint8_t partial_out[960]);
+bh_status bh_vk_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written);
+bh_status bh_proof_from_partials(const uint8_t* vk_bytes, size_t vk_len, const uint8_t* partials, size_t nshards,
+                                 const uint64_t r[4], const uint64_t s[4], uint8_t proof_out[192]);
+
+/* RCCL exchange (one communicator per rank/device; unique id shared out of band) */
+typedef struct bh_comm bh_comm;
+bh_status bh_comm_unique_id(uint8_t out[128]);
+bh_status bh_comm_init(bh_ctx* ctx, const uint8_t id[128], int nranks, int rank, bh_comm** out);
+/* all ranks' records, rank order: all_out holds nranks * BH_PARTIAL_BYTES bytes */
+bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t* all_out);
+bh_status bh_comm_destroy(bh_comm* c);
+bh_status bh_ctx_synchronize(bh_ctx* ctx);
+int bh_device_count(void);
+
 /* ---- synthetic workload: MiMC chain (mimc_mod.rs:40-130 with R rounds, seeded constants),
  * synthesized natively (witness) and its CRS generated on the device with the classic
  * algorithm (generator.rs:310-572) from the given toxic waste (canonical u64 each). */

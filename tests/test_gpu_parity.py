@@ -238,3 +238,15 @@ def test_native_chain_params_and_witness(ctx, golden, name, rounds):
     assert params.write().hex() == fx["params"]
     w = bh.Witness.chain(ctx, rounds)
     assert bh.prove_witness(ctx, params, w, 27134, 17146).hex() == fx["proof"]
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_sharded_partials_combine(ctx, golden, nshards):
+    """The multi-GPU decomposition on one device: per-shard partial multiexps
+    (bh_prove_witness_partial) summed by bh_proof_from_partials give the proof."""
+    bh = _bh()
+    fx = [f for f in golden["proofs"] if f["name"] == "mimc_chain_r15"][0]
+    params = bh.Parameters.chain(ctx, 15)
+    w = bh.Witness.chain(ctx, 15)
+    parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, nshards) for k in range(nshards))
+    assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146).hex() == fx["proof"]
