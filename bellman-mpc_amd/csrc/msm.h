@@ -24,7 +24,9 @@ template <class C>
 struct MsmWorkspace {
   size_t cap_n = 0, cap_E = 0, cap_nbt = 0, cap_segs = 0, cap_T = 0;
   uint32_t *entries = nullptr, *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *scan_scratch = nullptr,
-           *cont_bucket = nullptr;
+           *cont_bucket = nullptr, *tilecounts = nullptr, *tscan = nullptr;
+  uint2* recs = nullptr;
+  size_t cap_tc = 0;
   typename C::P *bucket_sums = nullptr, *conts = nullptr, *seg_weighted = nullptr, *seg_sum = nullptr,
                 *window_sums = nullptr;
   typename C::P* host_window_sums = nullptr;  // pinned, W entries after the stream completes
@@ -57,4 +59,10 @@ hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx
                        uint32_t* counts, hipStream_t st);
 hipError_t launch_scatter(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
                           const MsmShape& sh, uint32_t* cursor, uint32_t* entries, hipStream_t st);
+// LDS radix-partition sort of the (window, bucket) entries; fills entries, counts[0..nbt),
+// offsets[0..nbt] (offsets[nbt] = E)
+size_t sort_tilecount_words(const MsmShape& sh, size_t n);
+hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
+                        const MsmShape& sh, uint32_t* tilecounts, uint32_t* tscan_scratch, uint2* recs,
+                        uint32_t* entries, uint32_t* counts, uint32_t* offsets, hipStream_t st);
 }  // namespace bh

@@ -235,6 +235,161 @@ MsmShape msm_shape(size_t n, int c_override) {
   return sh;
 }
 
+// ----------------------------------------------------------------- LDS radix partition sort
+// Entries are keyed by the global bucket id gb = w*NB + |d|-1 (< nbt).  Pass 1 counts,
+// per tile of PT_TILE scalars, how many entries fall in each coarse partition
+// p = gb >> lo_bits (<= 4096 partitions, LDS histogram); a scan turns the
+// partition-major counts into offsets; pass 3 scatters (entry, gb & lo_mask)
+// records with LDS cursors; pass 4 (one workgroup per partition) sorts its
+// records by the low bits with an LDS counting sort and writes the final entry
+// array plus counts[gb] / offsets[gb] for every bucket of the partition.
+static constexpr int PT_TILE = 4096;  // scalars per tile
+
+__global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, size_t n, const int32_t* idx,
+                                                    DigitCfg cfg, int lo_bits, uint32_t P, uint32_t ntiles,
+                                                    uint32_t* tilecounts) {
+  extern __shared__ uint32_t hist[];
+  for (uint32_t i = threadIdx.x; i < P; i += 256) hist[i] = 0;
+  __syncthreads();
+  const size_t s0 = (size_t)blockIdx.x * PT_TILE;
+  const size_t s1 = min(s0 + PT_TILE, n);
+  for (size_t s = s0 + threadIdx.x; s < s1; s += 256) {
+    if (idx && idx[s] < 0) continue;
+    uint32_t sc[8];
+    load_scalar(scalars, s, sc);
+    uint32_t carry = 0;
+    for (int w = 0; w < cfg.W; w++) {
+      const int d = digit_at(sc, w, cfg.c, carry);
+      if (d != 0) {
+        const uint32_t gb = (uint32_t)w * cfg.NB + (uint32_t)(d < 0 ? -d : d) - 1u;
+        atomicAdd(&hist[gb >> lo_bits], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < P; p += 256) tilecounts[(size_t)p * ntiles + blockIdx.x] = hist[p];
+}
+
+__global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, size_t n, const int32_t* idx,
+                                                      uint32_t base_offset, DigitCfg cfg, int lo_bits, uint32_t P,
+                                                      uint32_t ntiles, const uint32_t* offs, uint2* recs) {
+  extern __shared__ uint32_t cur[];
+  for (uint32_t p = threadIdx.x; p < P; p += 256) cur[p] = offs[(size_t)p * ntiles + blockIdx.x];
+  __syncthreads();
+  const uint32_t lo_mask = (1u << lo_bits) - 1u;
+  const size_t s0 = (size_t)blockIdx.x * PT_TILE;
+  const size_t s1 = min(s0 + PT_TILE, n);
+  for (size_t s = s0 + threadIdx.x; s < s1; s += 256) {
+    uint32_t base;
+    if (idx) {
+      const int32_t v = idx[s];
+      if (v < 0) continue;
+      base = (uint32_t)v;
+    } else {
+      base = base_offset + (uint32_t)s;
+    }
+    uint32_t sc[8];
+    load_scalar(scalars, s, sc);
+    uint32_t carry = 0;
+    for (int w = 0; w < cfg.W; w++) {
+      const int d = digit_at(sc, w, cfg.c, carry);
+      if (d != 0) {
+        const uint32_t gb = (uint32_t)w * cfg.NB + (uint32_t)(d < 0 ? -d : d) - 1u;
+        const uint32_t pos = atomicAdd(&cur[gb >> lo_bits], 1u);
+        recs[pos] = make_uint2(base | (d < 0 ? 0x80000000u : 0u), gb & lo_mask);
+      }
+    }
+  }
+}
+
+// one workgroup per partition; bins = 2^lo_bits <= 4096
+__global__ void __launch_bounds__(256) k_part_sort(const uint2* recs, const uint32_t* offs, uint32_t ntiles,
+                                                   uint32_t P, int lo_bits, uint32_t nbt, uint32_t* entries,
+                                                   uint32_t* counts, uint32_t* offsets) {
+  __shared__ uint32_t bins[4096];
+  __shared__ uint32_t part[256];
+  const uint32_t p = blockIdx.x;
+  const uint32_t nb = 1u << lo_bits;
+  const uint32_t start = offs[(size_t)p * ntiles];
+  const uint32_t end = offs[(size_t)(p + 1) * ntiles];  // offs has P*ntiles+1 entries
+  for (uint32_t i = threadIdx.x; i < nb; i += 256) bins[i] = 0;
+  __syncthreads();
+  for (uint32_t j = start + threadIdx.x; j < end; j += 256) atomicAdd(&bins[recs[j].y], 1u);
+  __syncthreads();
+  // exclusive scan of bins: each thread owns a contiguous run of nb/256 (or 1) bins
+  const uint32_t per = (nb + 255) / 256;
+  const uint32_t b0 = threadIdx.x * per;
+  uint32_t local = 0;
+  for (uint32_t k = 0; k < per; k++) if (b0 + k < nb) local += bins[b0 + k];
+  part[threadIdx.x] = local;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    uint32_t t = (threadIdx.x >= (unsigned)off) ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  uint32_t run = start + part[threadIdx.x] - local;
+  for (uint32_t k = 0; k < per; k++) {
+    const uint32_t b = b0 + k;
+    if (b >= nb) break;
+    const uint32_t cnt = bins[b];
+    const uint32_t gb = (p << lo_bits) + b;
+    if (gb < nbt) { counts[gb] = cnt; offsets[gb] = run; }
+    bins[b] = run;  // becomes the write cursor
+    run += cnt;
+  }
+  if (p == P - 1 && threadIdx.x == 0) offsets[nbt] = end;
+  __syncthreads();
+  for (uint32_t j = start + threadIdx.x; j < end; j += 256) {
+    const uint2 r = recs[j];
+    const uint32_t pos = atomicAdd(&bins[r.y], 1u);
+    entries[pos] = r.x;
+  }
+}
+
+void sort_geometry(const MsmShape& sh, size_t n, int* lo_bits, uint32_t* P, uint32_t* ntiles) {
+  const size_t nbt = (size_t)sh.W * sh.NB;
+  int bits = 0;
+  while (((size_t)1 << bits) < nbt) bits++;
+  int lo = bits > 12 ? bits - 12 : 0;
+  *lo_bits = lo;
+  *P = (uint32_t)((nbt + ((size_t)1 << lo) - 1) >> lo);
+  *ntiles = (uint32_t)std::max<size_t>(1, (n + PT_TILE - 1) / PT_TILE);
+}
+
+size_t sort_tilecount_words(const MsmShape& sh, size_t n) {
+  int lo;
+  uint32_t P, nt;
+  sort_geometry(sh, n, &lo, &P, &nt);
+  return (size_t)P * nt + 1;
+}
+
+// counts/offsets (nbt+1 words) and the sorted entry array for one MSM
+hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
+                        const MsmShape& sh, uint32_t* tilecounts, uint32_t* tscan_scratch, uint2* recs,
+                        uint32_t* entries, uint32_t* counts, uint32_t* offsets, hipStream_t st) {
+  const size_t nbt = (size_t)sh.W * sh.NB;
+  DigitCfg cfg{sh.c, sh.W, sh.NB};
+  int lo;
+  uint32_t P, nt;
+  sort_geometry(sh, n, &lo, &P, &nt);
+  const size_t tw = (size_t)P * nt + 1;
+  hipMemsetAsync(tilecounts + tw - 1, 0, 4, st);
+  if (n == 0) {
+    hipMemsetAsync(counts, 0, (nbt + 1) * 4, st);
+    hipMemsetAsync(offsets, 0, (nbt + 1) * 4, st);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_part_count, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, cfg, lo, P, nt, tilecounts);
+  exclusive_scan(tilecounts, tilecounts, tw, tscan_scratch, st);
+  hipLaunchKernelGGL(k_part_scatter, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, base_offset, cfg, lo, P,
+                     nt, tilecounts, recs);
+  hipLaunchKernelGGL(k_part_sort, dim3(P), dim3(256), 0, st, recs, tilecounts, nt, P, lo, (uint32_t)nbt, entries,
+                     counts, offsets);
+  return hipGetLastError();
+}
+
 hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, const MsmShape& sh,
                        uint32_t* counts, hipStream_t st) {
   if (n == 0) return hipSuccess;

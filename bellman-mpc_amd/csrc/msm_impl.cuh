@@ -199,8 +199,11 @@ hipError_t MsmWorkspace<C>::grow(size_t E, size_t nbt, size_t segs, size_t T) {
   hipError_t err;
   if (E > cap_E) {
     if (entries) hipFree(entries);
+    if (recs) hipFree(recs);
     entries = nullptr;
+    recs = nullptr;
     if ((err = hipMalloc(&entries, std::max<size_t>(E, 1) * 4)) != hipSuccess) return err;
+    if ((err = hipMalloc(&recs, std::max<size_t>(E, 1) * 8)) != hipSuccess) return err;
     cap_E = E;
   }
   if (nbt > cap_nbt) {
@@ -249,6 +252,16 @@ hipError_t MsmWorkspace<C>::reserve_shape(size_t n, const MsmShape& sh) {
   const size_t nbt = (size_t)sh.W * sh.NB;
   const size_t segs = (E + sh.S - 1) / sh.S + 1;
   const size_t T = (size_t)sh.W * (sh.NB / sh.L);
+  const size_t tc = sort_tilecount_words(sh, n);
+  if (tc > cap_tc) {
+    if (tilecounts) hipFree(tilecounts);
+    if (tscan) hipFree(tscan);
+    tilecounts = tscan = nullptr;
+    hipError_t err;
+    if ((err = hipMalloc(&tilecounts, tc * 4)) != hipSuccess) return err;
+    if ((err = hipMalloc(&tscan, scan_scratch_words(tc) * 4 + 64)) != hipSuccess) return err;
+    cap_tc = tc;
+  }
   return grow(E, nbt, segs, T);
 }
 
@@ -268,6 +281,12 @@ hipError_t MsmWorkspace<C>::reserve(size_t n_max) {
 template <class C>
 void MsmWorkspace<C>::release() {
   if (entries) hipFree(entries);
+  if (recs) hipFree(recs);
+  if (tilecounts) hipFree(tilecounts);
+  if (tscan) hipFree(tscan);
+  recs = nullptr;
+  tilecounts = tscan = nullptr;
+  cap_tc = 0;
   if (counts) hipFree(counts);
   if (offsets) hipFree(offsets);
   if (cursor) hipFree(cursor);
@@ -295,12 +314,9 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
     if (e != hipSuccess) return e;
   }
   const size_t nbt = (size_t)sh.W * sh.NB;
-  hipMemsetAsync(ws.counts, 0, (nbt + 1) * 4, st);
-  launch_hist(d_scalars, n, d_idx, sh, ws.counts, st);
-  exclusive_scan(ws.counts, ws.offsets, nbt + 1, ws.scan_scratch, st);
-  hipMemcpyAsync(ws.cursor, ws.offsets, (nbt + 1) * 4, hipMemcpyDeviceToDevice, st);
+  sort_entries(d_scalars, n, d_idx, base_offset, sh, ws.tilecounts, ws.tscan, ws.recs, ws.entries, ws.counts,
+               ws.offsets, st);
   if (n > 0) {
-    launch_scatter(d_scalars, n, d_idx, base_offset, sh, ws.cursor, ws.entries, st);
     const size_t Emax = n * (size_t)sh.W;
     const size_t segs = (Emax + sh.S - 1) / sh.S;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
