@@ -516,8 +516,16 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   bh_ctx* c = new bh_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  for (auto& e : c->jev)
+    if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess) {
+    delete c;
+    return BH_ERR_OUT_OF_MEMORY;
+  }
   *out = c;
   return BH_OK;
 }
@@ -526,11 +534,18 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (!ctx) return BH_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream2);
   ctx->g1ws.release();
   ctx->g2ws.release();
+  ctx->g1ws_b.release();
+  ctx->g2ws_b.release();
   ctx->domains.clear();
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->jev) if (e) (void)hipEventDestroy(e);
+  if (ctx->host_out1) (void)hipHostFree(ctx->host_out1);
+  if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
   (void)hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->stream2);
   delete ctx;
   return BH_OK;
 }
@@ -542,6 +557,8 @@ bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domai
   if (max_msm_len) {
     BH_TRY_HIP(ctx->g1ws.reserve(max_msm_len));
     BH_TRY_HIP(ctx->g2ws.reserve(max_msm_len));
+    BH_TRY_HIP(ctx->g1ws_b.reserve(max_msm_len));
+    BH_TRY_HIP(ctx->g2ws_b.reserve(max_msm_len));
   }
   size_t n = std::max(max_msm_len, (size_t)1 << max_log_domain);
   BH_TRY_HIP(ctx->staging.alloc(n * 32));

@@ -90,9 +90,15 @@ struct bh_witness {
 struct bh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // reduction tails of pipelined multiexps
   int window_override = 0;
   bh::MsmWorkspace<G1Ops> g1ws;
   bh::MsmWorkspace<G2Ops> g2ws;
+  bh::MsmWorkspace<G1Ops> g1ws_b;  // second slot for the prover's ping-pong pipeline
+  bh::MsmWorkspace<G2Ops> g2ws_b;
+  XYZZ<FpOps>* host_out1 = nullptr;   // pinned, 8 jobs x 128 windows (c >= 2)
+  XYZZ<Fp2Ops>* host_out2 = nullptr;  // pinned, 2 jobs x 128 windows
+  hipEvent_t jev[48] = {};
   std::map<int, std::unique_ptr<bh::Domain>> domains;
   bh::DevBuf staging;     // generic host->device staging (scalars, polynomials)
   bh::DevBuf staging2;
@@ -100,6 +106,7 @@ struct bh_ctx {
   bh::DevBuf dtmp;        // density scan tmp
   bh::DevBuf dscan;       // scan scratch
   bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
+  bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
   double last_timings[8] = {};
   std::mutex mu;

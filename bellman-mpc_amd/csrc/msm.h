@@ -46,6 +46,14 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
                            size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
                            MsmTiming* timing);
 
+// The same MSM split in two stream-ordered halves: front = digit sort + bucket
+// accumulation, back = bucket reduction + window sums -> host_out (pinned, W entries).
+template <class C>
+hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                     size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing);
+template <class C>
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, typename C::P* host_out);
+
 size_t scan_scratch_words(size_t n);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st);
 hipError_t scalars_prepare(const uint32_t* d_in, uint32_t* d_out, size_t n, int mode, int log_perm, hipStream_t st);

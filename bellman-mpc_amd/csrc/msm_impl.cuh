@@ -305,10 +305,10 @@ void MsmWorkspace<C>::release() {
   cap_n = cap_E = cap_nbt = cap_segs = cap_T = 0;
 }
 
+// Front half: sort the digits and accumulate the buckets (stream `st`).
 template <class C>
-hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
-                           size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
-                           MsmTiming* timing) {
+hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                     size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing) {
   {
     hipError_t e = ws.reserve_shape(n, sh);
     if (e != hipSuccess) return e;
@@ -328,6 +328,12 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
       hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
                          ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   }
+  return hipGetLastError();
+}
+
+// Back half: summation by parts and the per-window sums, copied to host_out (W entries).
+template <class C>
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, typename C::P* host_out) {
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
   const size_t total = (size_t)sh.W * T;
   hipLaunchKernelGGL(k_bucket_reduce<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
@@ -337,8 +343,19 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
                      (uint32_t)sh.L, (uint32_t)total);
   constexpr int TB = std::is_same<C, G1Ops>::value ? 128 : 64;
   hipLaunchKernelGGL((k_tree_reduce<C, TB>), dim3(sh.W), dim3(TB), 0, st, ws.seg_weighted, T, ws.window_sums);
-  hipMemcpyAsync(ws.host_window_sums, ws.window_sums, sh.W * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+  hipMemcpyAsync(host_out, ws.window_sums, sh.W * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
   return hipGetLastError();
+}
+
+template <class C>
+hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                           size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
+                           MsmTiming* timing) {
+  hipError_t e = msm_front<C>(ws, st, d_bases, d_scalars, n, d_idx, base_offset, sh, timing);
+  if (e != hipSuccess) return e;
+  e = ws.reserve_shape(n, sh);
+  if (e != hipSuccess) return e;
+  return msm_back<C>(ws, st, sh, ws.host_window_sums);
 }
 
 }  // namespace bh

@@ -283,47 +283,100 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, ctx->stream));
   hipEventRecord(ctx->ev[1], ctx->stream);
 
+  // ---- the 8 multiexps (prover.rs:233-307), pipelined: job j's sort + accumulation
+  // run on stream A while job j-1's bucket reduction runs on stream B (ping-pong
+  // workspaces per curve); the host Horner-combines every job at the end.
+  const uint32_t* inputs = w->inputs.as<uint32_t>();
+  const uint32_t* aux = w->aux.as<uint32_t>();
+  BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
+  int32_t* idx_aaux = ctx->idx3.as<int32_t>();
+  int32_t* idx_bin = idx_aaux + na;
+  int32_t* idx_baux = idx_bin + ni;
+  if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
+                                   ctx->dscan.as<uint32_t>(), ctx->stream));
+  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(),
+                                   ctx->stream));
+  if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx_baux, ctx->dtmp.as<uint32_t>(),
+                                   ctx->dscan.as<uint32_t>(), ctx->stream));
+  struct Job {
+    bool g2;
+    const bh_srs* srs;
+    size_t base_off;       // used when idx == nullptr
+    const uint32_t* sc;
+    size_t n;              // full query length (sharded below)
+    const int32_t* idx;
+    size_t used;           // density-set scalars (roofline accounting)
+    int out;               // result slot: G1 0..5 / G2 0..1
+  };
+  // the big G2 job first so its (longest) tail hides under G1 accumulation
+  const Job jobs[8] = {
+      {true, &params->b_g2, 0, aux, na, idx_baux, w->b_aux_total, 1},      // b_g2_aux
+      {false, &params->h, 0, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
+      {false, &params->l, 0, aux, na, nullptr, na, 1},                     // l
+      {false, &params->a, 0, aux, na, idx_aaux, w->a_aux_total, 3},        // a_aux
+      {false, &params->b_g1, 0, aux, na, idx_baux, w->b_aux_total, 5},     // b_g1_aux
+      {false, &params->a, 0, inputs, ni, nullptr, ni, 2},                  // a_inputs
+      {false, &params->b_g1, 0, inputs, ni, idx_bin, w->b_in_total, 4},    // b_g1_inputs
+      {true, &params->b_g2, 0, inputs, ni, idx_bin, w->b_in_total, 0},     // b_g2_inputs
+  };
+  MsmWorkspace<G1Ops>* ws1[2] = {&ctx->g1ws, &ctx->g1ws_b};
+  MsmWorkspace<G2Ops>* ws2[2] = {&ctx->g2ws, &ctx->g2ws_b};
+  hipEvent_t* back_done = ctx->jev + 40;  // [g1 slot0, g1 slot1, g2 slot0, g2 slot1]
+  bool used_slot[4] = {false, false, false, false};
+  int next1 = 0, next2 = 0;
+  MsmShape shapes[8];
+  bool ran[8] = {false};
+  size_t lo, hi;
+  for (int j = 0; j < 8; j++) {
+    const Job& J = jobs[j];
+    shard_range(J.n, shard, nshards, &lo, &hi);
+    if (hi <= lo) continue;
+    const size_t n = hi - lo;
+    const MsmShape sh = msm_shape(n, ctx->window_override);
+    shapes[j] = sh;
+    ran[j] = true;
+    const int slot = J.g2 ? next2 : next1;
+    const int ev_slot = (J.g2 ? 2 : 0) + slot;
+    if (used_slot[ev_slot]) BH_TRY_HIP(hipStreamWaitEvent(ctx->stream, back_done[ev_slot], 0));
+    MsmTiming tm;
+    tm.ev_acc_begin = ctx->jev[2 * j];
+    tm.ev_acc_end = ctx->jev[2 * j + 1];
+    const uint32_t* bases = J.srs->pts.as<uint32_t>();
+    const int32_t* ix = J.idx ? J.idx + lo : nullptr;
+    const uint32_t boff = (uint32_t)(J.base_off + lo);
+    if (J.g2) BH_TRY_HIP(msm_front<G2Ops>(*ws2[slot], ctx->stream, bases, J.sc + lo * 8, n, ix, boff, sh, &tm));
+    else BH_TRY_HIP(msm_front<G1Ops>(*ws1[slot], ctx->stream, bases, J.sc + lo * 8, n, ix, boff, sh, &tm));
+    BH_TRY_HIP(hipEventRecord(ctx->jev[16 + j], ctx->stream));
+    BH_TRY_HIP(hipStreamWaitEvent(ctx->stream2, ctx->jev[16 + j], 0));
+    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(*ws2[slot], ctx->stream2, sh, ctx->host_out2 + 128 * J.out));
+    else BH_TRY_HIP(msm_back<G1Ops>(*ws1[slot], ctx->stream2, sh, ctx->host_out1 + 128 * J.out));
+    BH_TRY_HIP(hipEventRecord(back_done[ev_slot], ctx->stream2));
+    used_slot[ev_slot] = true;
+    if (J.g2) next2 ^= 1;
+    else next1 ^= 1;
+  }
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream2));
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0;
   int g1_launches = 0, g2_launches = 0;
-  const uint32_t* inputs = w->inputs.as<uint32_t>();
-  const uint32_t* aux = w->aux.as<uint32_t>();
-  int32_t* idx = ctx->idx.as<int32_t>();
-  size_t lo, hi;
-  // one sharded G1 multiexp: scalars [lo,hi) of an n-vector; idx (if any) maps the full vector
-  auto g1 = [&](const bh_srs* srs, size_t base_off, const uint32_t* sc, size_t n, const int32_t* ix, size_t used,
-                Jac<Fp>* out) -> bh_status {
-    shard_range(n, shard, nshards, &lo, &hi);
-    bh_status st = msm_g1_device(ctx, srs, base_off + lo, sc + lo * 8, hi - lo, ix ? ix + lo : nullptr, out,
-                                 &g1_acc_ms);
-    if (hi > lo) { g1_launches++; g1_pairs += (size_t)((unsigned __int128)used * (hi - lo) / std::max<size_t>(n, 1)); }
-    return st;
-  };
-  auto g2 = [&](const bh_srs* srs, size_t base_off, const uint32_t* sc, size_t n, const int32_t* ix, size_t used,
-                Jac<bh::Fp2>* out) -> bh_status {
-    shard_range(n, shard, nshards, &lo, &hi);
-    bh_status st = msm_g2_device(ctx, srs, base_off + lo, sc + lo * 8, hi - lo, ix ? ix + lo : nullptr, out,
-                                 &g2_acc_ms);
-    if (hi > lo) { g2_launches++; g2_pairs += (size_t)((unsigned __int128)used * (hi - lo) / std::max<size_t>(n, 1)); }
-    return st;
-  };
-  // h: FullDensity over params.h (prover.rs:233)
-  if ((s = g1(&params->h, 0, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, &res1[0]))) return s;
-  // l: FullDensity over aux (prover.rs:252-257)
-  if ((s = g1(&params->l, 0, aux, na, nullptr, na, &res1[1]))) return s;
-  // a_inputs / a_aux (prover.rs:259-275)
-  if ((s = g1(&params->a, 0, inputs, ni, nullptr, ni, &res1[2]))) return s;
-  if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(),
-                                   ctx->stream));
-  if ((s = g1(&params->a, 0, aux, na, idx, w->a_aux_total, &res1[3]))) return s;
-  // b_g1 / b_g2 inputs (prover.rs:277-307)
-  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), ctx->stream));
-  if ((s = g1(&params->b_g1, 0, inputs, ni, idx, w->b_in_total, &res1[4]))) return s;
-  if ((s = g2(&params->b_g2, 0, inputs, ni, idx, w->b_in_total, &res2[0]))) return s;
-  if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx, ctx->dtmp.as<uint32_t>(),
-                                   ctx->dscan.as<uint32_t>(), ctx->stream));
-  if ((s = g1(&params->b_g1, 0, aux, na, idx, w->b_aux_total, &res1[5]))) return s;
-  if ((s = g2(&params->b_g2, 0, aux, na, idx, w->b_aux_total, &res2[1]))) return s;
+  for (int i = 0; i < 6; i++) res1[i] = jac_identity<Fp>();
+  for (int i = 0; i < 2; i++) res2[i] = jac_identity<bh::Fp2>();
+  for (int j = 0; j < 8; j++) {
+    if (!ran[j]) continue;
+    const Job& J = jobs[j];
+    float t = 0;
+    (void)hipEventElapsedTime(&t, ctx->jev[2 * j], ctx->jev[2 * j + 1]);
+    shard_range(J.n, shard, nshards, &lo, &hi);
+    const size_t pairs = (size_t)((unsigned __int128)J.used * (hi - lo) / std::max<size_t>(J.n, 1));
+    if (J.g2) {
+      res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].W, shapes[j].c);
+      g2_acc_ms += t; g2_launches++; g2_pairs += pairs;
+    } else {
+      res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j].W, shapes[j].c);
+      g1_acc_ms += t; g1_launches++; g1_pairs += pairs;
+    }
+  }
 
   const auto t1 = std::chrono::steady_clock::now();
   float h_ms = 0;
