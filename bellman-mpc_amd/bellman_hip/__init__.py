@@ -112,6 +112,8 @@ def _load():
         "bh_comm_destroy": (I, [P]),
         "bh_ctx_synchronize": (I, [P]),
         "bh_device_count": (I, []),
+        "bh_ctx_set_tables": (I, [P, I]),
+        "bh_params_prepare": (I, [P, P, P, S]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -131,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "bh_prove", "bh_witness_upload", "bh_witness_free", "bh_prove_witness", "bh_chain_witness",
     "bh_chain_params", "bh_params_write", "bh_last_timings", "bh_shard_range", "bh_prove_witness_partial",
     "bh_vk_write", "bh_proof_from_partials", "bh_comm_unique_id", "bh_comm_init", "bh_comm_allgather_partials",
-    "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count",
+    "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count", "bh_ctx_set_tables", "bh_params_prepare",
 ]
 PARTIAL_BYTES = 960
 
@@ -205,6 +207,10 @@ class Context:
 
     def set_window(self, c):
         _check(_lib.bh_ctx_set_window(self.h, c), "bh_ctx_set_window")
+
+    def set_tables(self, enable):
+        """Prover SRS window tables on/off (results never depend on it)."""
+        _check(_lib.bh_ctx_set_tables(self.h, int(bool(enable))), "bh_ctx_set_tables")
 
     def synchronize(self):
         _check(_lib.bh_ctx_synchronize(self.h))
@@ -375,6 +381,10 @@ class Parameters:
         out = np.zeros(n.value, dtype=np.uint8)
         _check(_lib.bh_params_write(self.h, _ptr(out), n.value, ctypes.byref(n)))
         return out.tobytes()
+
+    def prepare(self, witness, nshards=1):
+        """Build the prover window tables now rather than inside the first proof."""
+        _check(_lib.bh_params_prepare(self.ctx.h, self.h, witness.h, nshards), "bh_params_prepare")
 
     def vk_bytes(self):
         """VerifyingKey::write (groth16/mod.rs:146-159)."""

@@ -1,6 +1,7 @@
 // C ABI implementation: context, bases (SRS), multiexp, EvaluationDomain,
 // Parameters and the Groth16 prover core.  See include/bellman_hip.h for the
 // reference interface each entry point replaces.
+#include <cstdlib>
 #include <string.h>
 
 #include <algorithm>
@@ -462,7 +463,7 @@ static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind
 
 // H pipeline on device-resident a|b|c (3*m packed device form, natural order). On return
 // d_abc's first m entries hold h coefficients in BIT-REVERSED order (device form).
-bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc) {
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st) {
   const int L = D->L;
   const size_t m = (size_t)1 << L;
   uint32_t* a = d_abc;
@@ -472,14 +473,14 @@ bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc) {
   // then fft (DIT, bit-reversed -> natural) = coset_fft
   for (uint32_t* x : {a, b, c}) {
     launch_ntt(x, L, true, D->tw_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
-               D->lo_bits, ctx->stream);
-    launch_ntt(x, L, false, D->tw_fwd.as<uint32_t>(), nullptr, nullptr, 0, ctx->stream);
+               D->lo_bits, st);
+    launch_ntt(x, L, false, D->tw_fwd.as<uint32_t>(), nullptr, nullptr, 0, st);
   }
   // prover.rs:221-225: a*b - c, divide_by_z_on_coset
-  launch_pointwise(a, b, c, m, 2, D->consts.as<uint32_t>() + 9, ctx->stream);
+  launch_pointwise(a, b, c, m, 2, D->consts.as<uint32_t>() + 9, st);
   // prover.rs:226: icoset_fft = ifft + distribute_powers(g^-1), fused as above (output bit-reversed)
   launch_ntt(a, L, true, D->tw_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
-             D->lo_bits, ctx->stream);
+             D->lo_bits, st);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
 }
@@ -516,7 +517,16 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   bh_ctx* c = new bh_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
-  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  const char* pe = getenv("BH_SIDE_PRIORITY");  // experiment knob: 1 = side streams at high priority
+  const int side = (pe && pe[0] == '1') ? prio_hi : prio_lo;
+  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return BH_ERR_HIP;
+  }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
@@ -535,10 +545,12 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->stream2);
+  (void)hipStreamSynchronize(ctx->stream3);
+  (void)hipStreamSynchronize(ctx->stream4);
   ctx->g1ws.release();
   ctx->g2ws.release();
-  ctx->g1ws_b.release();
-  ctx->g2ws_b.release();
+  for (auto& w : ctx->pw1) w.release();
+  for (auto& w : ctx->pw2) w.release();
   ctx->domains.clear();
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->jev) if (e) (void)hipEventDestroy(e);
@@ -546,6 +558,8 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->stream2);
+  (void)hipStreamDestroy(ctx->stream3);
+  (void)hipStreamDestroy(ctx->stream4);
   delete ctx;
   return BH_OK;
 }
@@ -557,8 +571,6 @@ bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domai
   if (max_msm_len) {
     BH_TRY_HIP(ctx->g1ws.reserve(max_msm_len));
     BH_TRY_HIP(ctx->g2ws.reserve(max_msm_len));
-    BH_TRY_HIP(ctx->g1ws_b.reserve(max_msm_len));
-    BH_TRY_HIP(ctx->g2ws_b.reserve(max_msm_len));
   }
   size_t n = std::max(max_msm_len, (size_t)1 << max_log_domain);
   BH_TRY_HIP(ctx->staging.alloc(n * 32));
@@ -572,6 +584,12 @@ bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domai
     bh_status s = ctx_domain(ctx, (int)max_log_domain, &D);
     if (s) return s;
   }
+  return BH_OK;
+}
+
+bh_status bh_ctx_set_tables(bh_ctx* ctx, int enable) {
+  if (!ctx || (enable != 0 && enable != 1)) return BH_ERR_INVALID_ARGUMENT;
+  ctx->tables = enable;
   return BH_OK;
 }
 
@@ -761,7 +779,7 @@ bh_status bh_compute_h(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const 
   if ((s = upload_fr(ctx, a, nc, m, abc))) return s;
   if ((s = upload_fr(ctx, b, nc, m, abc + m * 8))) return s;
   if ((s = upload_fr(ctx, c, nc, m, abc + 2 * m * 8))) return s;
-  if ((s = run_h_pipeline(ctx, D, abc))) return s;
+  if ((s = run_h_pipeline(ctx, D, abc, ctx->stream))) return s;
   // bit-reversed -> natural
   launch_permute(abc, ctx->staging2.as<uint32_t>(), (int)L, nullptr, nullptr, 0, ctx->stream);
   if ((s = download_fr(ctx, ctx->staging2.as<uint32_t>(), m - 1, h_out))) return s;

@@ -40,6 +40,11 @@ struct DevBuf {
     if (e == hipSuccess) bytes = b;
     return e;
   }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
@@ -64,6 +69,10 @@ struct bh_srs {
   size_t n = 0;
   bh::DevBuf pts;                    // packed affine, device Montgomery
   std::vector<size_t> identity_idx;  // indices of points at infinity (rejected by next())
+  // prover window table (built lazily, see prepare_tables in prover.hip):
+  // win[i*win_W + w] = 2^(win_c*w) * P_i, packed affine
+  bh::DevBuf win;
+  int win_c = 0, win_W = 0;
 };
 
 struct bh_params {
@@ -90,12 +99,17 @@ struct bh_witness {
 struct bh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t stream2 = nullptr;  // reduction tails of pipelined multiexps
+  hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
+  hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
+  hipStream_t stream4 = nullptr;  // prover: H pipeline
   int window_override = 0;
+  int tables = 1;  // 1: the prover builds and uses SRS window tables (bh_ctx_set_tables)
   bh::MsmWorkspace<G1Ops> g1ws;
   bh::MsmWorkspace<G2Ops> g2ws;
-  bh::MsmWorkspace<G1Ops> g1ws_b;  // second slot for the prover's ping-pong pipeline
-  bh::MsmWorkspace<G2Ops> g2ws_b;
+  // one workspace per prover multiexp (result slot order), so that sorts, accumulations and
+  // tails of different multiexps never share buffers (about 1 GB each at 2^22 points)
+  bh::MsmWorkspace<G1Ops> pw1[6];
+  bh::MsmWorkspace<G2Ops> pw2[2];
   XYZZ<FpOps>* host_out1 = nullptr;   // pinned, 8 jobs x 128 windows (c >= 2)
   XYZZ<Fp2Ops>* host_out2 = nullptr;  // pinned, 2 jobs x 128 windows
   hipEvent_t jev[48] = {};
@@ -128,7 +142,7 @@ bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, co
                         const int32_t* d_idx, Jac<Fp2>* out, float* acc_ms);
 bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst);
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
-bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc);
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,
                          bh_srs* out);
 // reference-exact error semantics of multiexp (EOF / identity), host side

@@ -11,6 +11,8 @@
 //                  trick), result packed canonical in the bh_srs layout.
 #include "crs.h"
 
+#include <algorithm>
+
 namespace bh {
 
 template <class C>
@@ -126,6 +128,53 @@ hipError_t fixed_base_batch(const uint32_t* d_table, const uint32_t* d_scalars, 
                      reinterpret_cast<typename FieldOf<C>::F::T*>(d_scratch), d_out);
   return hipGetLastError();
 }
+
+// t-th point of the chunk: its W window multiples, doubling c times between windows
+template <class C>
+__global__ void __launch_bounds__(256) k_window_multiples(const uint32_t* pts, size_t i0, size_t cnt, int c, int W,
+                                                          typename C::P* out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt) return;
+  typename C::P acc = C::from_affine(load_affine_packed<C>(pts, i0 + t));
+  out[t * W] = acc;
+  for (int w = 1; w < W; w++) {
+    for (int j = 0; j < c; j++) acc = C::dbl(acc);
+    out[t * W + w] = acc;
+  }
+}
+
+template <class C>
+size_t window_table_scratch_bytes(size_t chunk, int W) {
+  return chunk * (size_t)W * (sizeof(typename C::P) + sizeof(typename FieldOf<C>::F::T));
+}
+
+template <class C>
+hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t* d_out, void* d_scratch,
+                        size_t chunk, hipStream_t st) {
+  using P = typename C::P;
+  using T = typename FieldOf<C>::F::T;
+  constexpr int PW = FieldOf<C>::F::PACKED_WORDS;
+  constexpr int CHUNK = 32;
+  P* xyzz = reinterpret_cast<P*>(d_scratch);
+  T* prefix = reinterpret_cast<T*>(reinterpret_cast<char*>(d_scratch) + chunk * (size_t)W * sizeof(P));
+  for (size_t i0 = 0; i0 < n; i0 += chunk) {
+    const size_t cnt = std::min(chunk, n - i0);
+    hipLaunchKernelGGL(k_window_multiples<C>, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, d_pts, i0, cnt,
+                       c, W, xyzz);
+    const size_t m = cnt * (size_t)W;
+    const size_t threads = (m + CHUNK - 1) / CHUNK;
+    hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, xyzz, m,
+                       prefix, d_out + i0 * (size_t)W * 2 * PW);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template size_t window_table_scratch_bytes<G1Ops>(size_t, int);
+template size_t window_table_scratch_bytes<G2Ops>(size_t, int);
+template hipError_t window_table<G1Ops>(const uint32_t*, size_t, int, int, uint32_t*, void*, size_t, hipStream_t);
+template hipError_t window_table<G2Ops>(const uint32_t*, size_t, int, int, uint32_t*, void*, size_t, hipStream_t);
 
 template hipError_t fixed_base_batch<G1Ops>(const uint32_t*, const uint32_t*, size_t, void*, void*, uint32_t*,
                                             hipStream_t);

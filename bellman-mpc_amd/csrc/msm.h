@@ -8,13 +8,18 @@
 namespace bh {
 
 struct MsmShape {
-  int c;   // window bits
-  int W;   // windows = ceil(256 / c) (signed digits need one spare bit)
-  int NB;  // buckets per window = 2^(c-1)
-  int L;   // buckets per running-sum thread
-  int S;   // sorted entries per accumulation thread
+  int c;    // window bits
+  int W;    // digit windows = ceil(256 / c) (signed digits need one spare bit)
+  int NB;   // buckets per bucket window = 2^(c-1)
+  int L;    // buckets per running-sum thread
+  int S;    // sorted entries per accumulation thread
+  int Wb;   // bucket windows: W, or 1 with a window table (all windows share the buckets)
+  int pre;  // 1: bases are a window table T[i*W + w] = 2^(c*w) * P_i (entry = i*W + w)
 };
 MsmShape msm_shape(size_t n, int c_override);
+// shape for a window table: c from the cost model n*ceil(256/c) + ~6.5 * 2^(c-1)
+int msm_table_c(size_t n);
+MsmShape msm_shape_table(size_t n, int c);
 
 struct MsmTiming {
   hipEvent_t ev_acc_begin = nullptr, ev_acc_end = nullptr;  // bracket k_accumulate_dev
@@ -37,7 +42,7 @@ struct MsmWorkspace {
   void release();
 };
 
-// Enqueue an MSM on `st`; on completion ws.host_window_sums[0..W) hold the
+// Enqueue an MSM on `st`; on completion ws.host_window_sums[0..Wb) hold the
 // canonical XYZZ sum of every window (device Montgomery form).
 // d_scalars: n canonical scalars (8 LE u32 words each); d_idx: per-scalar base
 // index (-1 = density bit clear) or nullptr for idx = base_offset + i.
@@ -47,12 +52,18 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
                            MsmTiming* timing);
 
 // The same MSM split in two stream-ordered halves: front = digit sort + bucket
-// accumulation, back = bucket reduction + window sums -> host_out (pinned, W entries).
+// accumulation, back = bucket reduction + window sums -> host_out (pinned, Wb entries).
+template <class C>
+hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
+                    uint32_t base_offset, const MsmShape& sh);
+template <class C>
+hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, size_t n, const MsmShape& sh,
+                          MsmTiming* timing);
 template <class C>
 hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
                      size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing);
 template <class C>
-hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, typename C::P* host_out);
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out);
 
 size_t scan_scratch_words(size_t n);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st);
@@ -63,10 +74,6 @@ hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset
 }  // namespace bh
 
 namespace bh {
-hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, const MsmShape& sh,
-                       uint32_t* counts, hipStream_t st);
-hipError_t launch_scatter(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
-                          const MsmShape& sh, uint32_t* cursor, uint32_t* entries, hipStream_t st);
 // LDS radix-partition sort of the (window, bucket) entries; fills entries, counts[0..nbt),
 // offsets[0..nbt] (offsets[nbt] = E)
 size_t sort_tilecount_words(const MsmShape& sh, size_t n);

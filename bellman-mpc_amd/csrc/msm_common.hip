@@ -18,7 +18,7 @@
 //   k_bucket_reduce one thread per L consecutive buckets: running sums
 //               (summation by parts) -> (sum_t, weighted_t)
 //   k_seg_combine  weighted_t + (t*L)*sum_t
-//   k_tree_reduce  one workgroup per window: sum of the segment results
+//   k_sum_groups   per-window sum of the segment results, a 4-ary tree of launches
 // The host then performs the W-window Horner step (multiexp.rs:244-249).
 //
 // Semantics of the reference Source (multiexp.rs:45-86) are reproduced by the
@@ -134,8 +134,18 @@ __global__ void k_density_index(const uint64_t* words, const uint32_t* word_pref
 
 // ----------------------------------------------------------------- digits
 struct DigitCfg {
-  int c, W, NB;
+  int c, W, NB, pre;
 };
+
+// bucket id and entry of digit d of window w for base `base`
+__device__ __forceinline__ uint32_t digit_bucket(const DigitCfg& cfg, int w, int d) {
+  const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+  return cfg.pre ? b : (uint32_t)w * cfg.NB + b;
+}
+__device__ __forceinline__ uint32_t digit_entry(const DigitCfg& cfg, uint32_t base, int w, int d) {
+  const uint32_t e = cfg.pre ? base * (uint32_t)cfg.W + (uint32_t)w : base;
+  return e | (d < 0 ? 0x80000000u : 0u);
+}
 
 // signed digit of window w; returns digit in [-2^(c-1), 2^(c-1)], updates carry
 __device__ __forceinline__ int digit_at(const uint32_t* s, int w, int c, uint32_t& carry) {
@@ -159,49 +169,6 @@ __device__ __forceinline__ void load_scalar(const uint32_t* scalars, size_t i, u
   uint4 a = p[0], b = p[1];
   s[0] = a.x; s[1] = a.y; s[2] = a.z; s[3] = a.w;
   s[4] = b.x; s[5] = b.y; s[6] = b.z; s[7] = b.w;
-}
-
-__global__ void __launch_bounds__(256) k_hist(const uint32_t* scalars, size_t n, const int32_t* idx, DigitCfg cfg,
-                                              uint32_t* counts) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (idx && idx[i] < 0) return;
-  uint32_t s[8];
-  load_scalar(scalars, i, s);
-  uint32_t carry = 0;
-  for (int w = 0; w < cfg.W; w++) {
-    int d = digit_at(s, w, cfg.c, carry);
-    if (d != 0) {
-      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-      atomicAdd(&counts[(size_t)w * cfg.NB + b], 1u);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) k_scatter(const uint32_t* scalars, size_t n, const int32_t* idx,
-                                                 uint32_t base_offset, DigitCfg cfg, uint32_t* cursor,
-                                                 uint32_t* entries) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t base;
-  if (idx) {
-    const int32_t v = idx[i];
-    if (v < 0) return;
-    base = (uint32_t)v;
-  } else {
-    base = base_offset + (uint32_t)i;
-  }
-  uint32_t s[8];
-  load_scalar(scalars, i, s);
-  uint32_t carry = 0;
-  for (int w = 0; w < cfg.W; w++) {
-    int d = digit_at(s, w, cfg.c, carry);
-    if (d != 0) {
-      const uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
-      const uint32_t pos = atomicAdd(&cursor[(size_t)w * cfg.NB + b], 1u);
-      entries[pos] = base | (d < 0 ? 0x80000000u : 0u);
-    }
-  }
 }
 
 // Window choice: c ~ log2(n) - 6, clamped to [4, 16], preferring the c in
@@ -232,6 +199,28 @@ MsmShape msm_shape(size_t n, int c_override) {
   int S = 16;
   while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;
   sh.S = S;
+  sh.Wb = sh.W;
+  sh.pre = 0;
+  return sh;
+}
+
+// With a window table every digit window adds into one shared set of 2^(c-1) buckets, so
+// the accumulation costs n*ceil(256/c) mixed additions and the reduction ~6.5 * 2^(c-1)
+// (2 running-sum additions per bucket plus the segment combine), independent of W.
+int msm_table_c(size_t n) {
+  int best = 16;
+  double best_cost = 1e300;
+  for (int c = 8; c <= 22; c++) {
+    const double cost = (double)n * ((256 + c - 1) / c) + 6.5 * (double)((size_t)1 << (c - 1));
+    if (cost < best_cost) { best_cost = cost; best = c; }
+  }
+  return best;
+}
+
+MsmShape msm_shape_table(size_t n, int c) {
+  MsmShape sh = msm_shape(n, c);
+  sh.Wb = 1;
+  sh.pre = 1;
   return sh;
 }
 
@@ -260,10 +249,7 @@ __global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, siz
     uint32_t carry = 0;
     for (int w = 0; w < cfg.W; w++) {
       const int d = digit_at(sc, w, cfg.c, carry);
-      if (d != 0) {
-        const uint32_t gb = (uint32_t)w * cfg.NB + (uint32_t)(d < 0 ? -d : d) - 1u;
-        atomicAdd(&hist[gb >> lo_bits], 1u);
-      }
+      if (d != 0) atomicAdd(&hist[digit_bucket(cfg, w, d) >> lo_bits], 1u);
     }
   }
   __syncthreads();
@@ -294,9 +280,9 @@ __global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, s
     for (int w = 0; w < cfg.W; w++) {
       const int d = digit_at(sc, w, cfg.c, carry);
       if (d != 0) {
-        const uint32_t gb = (uint32_t)w * cfg.NB + (uint32_t)(d < 0 ? -d : d) - 1u;
+        const uint32_t gb = digit_bucket(cfg, w, d);
         const uint32_t pos = atomicAdd(&cur[gb >> lo_bits], 1u);
-        recs[pos] = make_uint2(base | (d < 0 ? 0x80000000u : 0u), gb & lo_mask);
+        recs[pos] = make_uint2(digit_entry(cfg, base, w, d), gb & lo_mask);
       }
     }
   }
@@ -349,7 +335,7 @@ __global__ void __launch_bounds__(256) k_part_sort(const uint2* recs, const uint
 }
 
 void sort_geometry(const MsmShape& sh, size_t n, int* lo_bits, uint32_t* P, uint32_t* ntiles) {
-  const size_t nbt = (size_t)sh.W * sh.NB;
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
   int bits = 0;
   while (((size_t)1 << bits) < nbt) bits++;
   int lo = bits > 12 ? bits - 12 : 0;
@@ -369,8 +355,8 @@ size_t sort_tilecount_words(const MsmShape& sh, size_t n) {
 hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
                         const MsmShape& sh, uint32_t* tilecounts, uint32_t* tscan_scratch, uint2* recs,
                         uint32_t* entries, uint32_t* counts, uint32_t* offsets, hipStream_t st) {
-  const size_t nbt = (size_t)sh.W * sh.NB;
-  DigitCfg cfg{sh.c, sh.W, sh.NB};
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
+  DigitCfg cfg{sh.c, sh.W, sh.NB, sh.pre};
   int lo;
   uint32_t P, nt;
   sort_geometry(sh, n, &lo, &P, &nt);
@@ -387,23 +373,6 @@ hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_id
                      nt, tilecounts, recs);
   hipLaunchKernelGGL(k_part_sort, dim3(P), dim3(256), 0, st, recs, tilecounts, nt, P, lo, (uint32_t)nbt, entries,
                      counts, offsets);
-  return hipGetLastError();
-}
-
-hipError_t launch_hist(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, const MsmShape& sh,
-                       uint32_t* counts, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  DigitCfg cfg{sh.c, sh.W, sh.NB};
-  hipLaunchKernelGGL(k_hist, dim3(blocks_for(n, 256)), dim3(256), 0, st, d_scalars, n, d_idx, cfg, counts);
-  return hipGetLastError();
-}
-
-hipError_t launch_scatter(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
-                          const MsmShape& sh, uint32_t* cursor, uint32_t* entries, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  DigitCfg cfg{sh.c, sh.W, sh.NB};
-  hipLaunchKernelGGL(k_scatter, dim3(blocks_for(n, 256)), dim3(256), 0, st, d_scalars, n, d_idx, base_offset, cfg,
-                     cursor, entries);
   return hipGetLastError();
 }
 

@@ -5,7 +5,11 @@ namespace bh {
 template struct MsmWorkspace<G1Ops>;
 template hipError_t msm_window_sums<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                          const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
+template hipError_t msm_sort<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, size_t, const int32_t*,
+                                     uint32_t, const MsmShape&);
+template hipError_t msm_accumulate<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,
+                                           MsmTiming*);
 template hipError_t msm_front<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
-template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const MsmShape&, typename G1Ops::P*);
+template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, size_t, const MsmShape&, typename G1Ops::P*);
 }  // namespace bh

@@ -1,6 +1,8 @@
 // Curve-generic MSM kernels and host driver (included once per curve by
 // msm_g1.hip / msm_g2.hip so the two instantiations compile in parallel).
 #pragma once
+#include <cstdlib>
+
 #include "msm.h"
 #include <algorithm>
 
@@ -134,20 +136,21 @@ __global__ void __launch_bounds__(256) k_seg_combine(typename C::P* seg_weighted
   store_point<C>(&seg_weighted[gid], v);
 }
 
-// one block per window: sum T points -> window_out[w] (canonical coordinates)
-template <class C, int BLOCK>
-__global__ void __launch_bounds__(BLOCK) k_tree_reduce(const typename C::P* pts, uint32_t T, typename C::P* window_out) {
-  __shared__ typename C::P sh[BLOCK];
-  const uint32_t w = blockIdx.x;
-  typename C::P acc = C::identity();
-  for (uint32_t t = threadIdx.x; t < T; t += BLOCK) acc = C::add(acc, load_point<C>(&pts[(size_t)w * T + t]));
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-  for (int off = BLOCK / 2; off > 0; off >>= 1) {
-    if ((int)threadIdx.x < off) sh[threadIdx.x] = C::add(sh[threadIdx.x], sh[threadIdx.x + off]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) window_out[w] = C::reduce(sh[0]);
+// one level of the per-window sum: out[w][t] = sum of in[w][t*G .. t*G+G) (G <= 4 keeps the
+// sequential chain short; the tail of the last multiexp is latency-bound).  The last level
+// (Tout == 1) writes canonical coordinates.
+template <class C>
+__global__ void __launch_bounds__(64) k_sum_groups(const typename C::P* in, uint32_t Tin, uint32_t G,
+                                                   typename C::P* out, uint32_t Tout, uint32_t W) {
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= W * Tout) return;
+  const uint32_t w = gid / Tout, t = gid % Tout;
+  const typename C::P* src = in + (size_t)w * Tin;
+  const uint32_t lo = t * G, hi = min(lo + G, Tin);
+  typename C::P acc = load_point<C>(&src[lo]);
+  for (uint32_t i = lo + 1; i < hi; i++) acc = C::add(acc, load_point<C>(&src[i]));
+  if (Tout == 1) out[w] = C::reduce(acc);
+  else store_point<C>(&out[gid], acc);
 }
 
 // The accumulate kernel needs E; it reads it from offsets[nbt] on device.
@@ -183,13 +186,88 @@ __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries,
   else store_point<C>(&conts[seg], acc);
 }
 
+// Same accumulation with the next entry's affine base prefetched global -> LDS by
+// global_load_lds_dwordx4 (no VGPR cost) while the current mixed addition runs: each wave
+// owns NQ x 64 x 16 B of LDS, lane l's base occupying slot l of each of the NQ rows.
+template <class C>
+__global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
+                                                       const uint32_t* bases, uint32_t S,
+                                                       typename C::P* bucket_sums, typename C::P* conts,
+                                                       uint32_t* cont_bucket) {
+  using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+  constexpr int PW = F::PACKED_WORDS;
+  constexpr int NQ = 2 * PW / 4;  // 16-byte pieces per affine base
+  __shared__ uint4 pre[4][NQ][64];
+  const uint32_t E = offsets[nbt];
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pos0 = seg * S;
+  if (pos0 >= E) return;
+  const uint32_t end = min(pos0 + S, E);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto issue = [&](uint32_t e) {
+    const uint32_t* src = bases + (size_t)(e & 0x7fffffffu) * 2 * PW;
+#pragma unroll
+    for (int q = 0; q < NQ; q++)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
+                                       (__attribute__((address_space(3))) void*)&pre[wv][q][0], 16, 0, 0);
+  };
+  uint32_t e_cur = entries[pos0];
+  issue(e_cur);
+  uint32_t e_next = (pos0 + 1 < end) ? entries[pos0 + 1] : 0u;
+  uint32_t b = find_bucket(offsets, nbt, pos0);
+  uint32_t next = offsets[b + 1];
+  bool started_here = offsets[b] >= pos0;
+  cont_bucket[seg] = started_here ? 0xffffffffu : b;
+  typename C::P acc = C::identity();
+  for (uint32_t j = pos0; j < end; j++) {
+    if (j == next) {
+      if (started_here) store_point<C>(&bucket_sums[b], acc);
+      else store_point<C>(&conts[seg], acc);
+      b++;
+      while (offsets[b + 1] <= j) b++;
+      next = offsets[b + 1];
+      started_here = true;
+      acc = C::identity();
+    }
+    __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
+    uint32_t w[2 * PW];
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const uint4 v = pre[wv][q][lane];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+    typename C::A a;
+    a.x = F::unpack(w);
+    a.y = F::unpack(w + PW);
+    if (e_cur & 0x80000000u) a = C::neg_affine(a);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
+    if (j + 1 < end) {
+      issue(e_next);
+      e_cur = e_next;
+      e_next = (j + 2 < end) ? entries[j + 2] : 0u;
+    }
+    acc = C::madd(acc, a);
+  }
+  if (started_here) store_point<C>(&bucket_sums[b], acc);
+  else store_point<C>(&conts[seg], acc);
+}
+
+// BH_ACC_PREFETCH=0 selects the register-load variant (A/B measurements only)
+inline int accumulate_variant() {
+  static int v = [] {
+    const char* e = getenv("BH_ACC_PREFETCH");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <class C>
 size_t MsmWorkspace<C>::bytes_needed(size_t n) {
   MsmShape sh = msm_shape(n, 0);
   size_t E = n * (size_t)sh.W;
-  size_t nbt = (size_t)sh.W * sh.NB;
+  size_t nbt = (size_t)sh.Wb * sh.NB;
   size_t segs = (E + sh.S - 1) / sh.S + 1;
-  size_t T = (size_t)sh.W * (sh.NB / sh.L);
+  size_t T = (size_t)sh.Wb * (sh.NB / sh.L);
   return E * 4 + nbt * 4 * 3 + 16 + nbt * sizeof(typename C::P) + segs * sizeof(typename C::P) +
          2 * T * sizeof(typename C::P) + n * 4;
 }
@@ -249,9 +327,9 @@ hipError_t MsmWorkspace<C>::grow(size_t E, size_t nbt, size_t segs, size_t T) {
 template <class C>
 hipError_t MsmWorkspace<C>::reserve_shape(size_t n, const MsmShape& sh) {
   const size_t E = n * (size_t)sh.W;
-  const size_t nbt = (size_t)sh.W * sh.NB;
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
   const size_t segs = (E + sh.S - 1) / sh.S + 1;
-  const size_t T = (size_t)sh.W * (sh.NB / sh.L);
+  const size_t T = (size_t)sh.Wb * (sh.NB / sh.L);
   const size_t tc = sort_tilecount_words(sh, n);
   if (tc > cap_tc) {
     if (tilecounts) hipFree(tilecounts);
@@ -307,43 +385,72 @@ void MsmWorkspace<C>::release() {
 
 // Front half: sort the digits and accumulate the buckets (stream `st`).
 template <class C>
-hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
-                     size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing) {
-  {
-    hipError_t e = ws.reserve_shape(n, sh);
-    if (e != hipSuccess) return e;
-  }
-  const size_t nbt = (size_t)sh.W * sh.NB;
+hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
+                    uint32_t base_offset, const MsmShape& sh) {
+  hipError_t e = ws.reserve_shape(n, sh);
+  if (e != hipSuccess) return e;
   sort_entries(d_scalars, n, d_idx, base_offset, sh, ws.tilecounts, ws.tscan, ws.recs, ws.entries, ws.counts,
                ws.offsets, st);
+  return hipGetLastError();
+}
+
+// bucket accumulation over the sorted entries
+template <class C>
+hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, size_t n, const MsmShape& sh,
+                          MsmTiming* timing) {
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
   if (n > 0) {
     const size_t Emax = n * (size_t)sh.W;
     const size_t segs = (Emax + sh.S - 1) / sh.S;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
-    hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries, ws.offsets,
-                       (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
+    if (accumulate_variant())
+      hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                         ws.offsets, (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
+    else
+      hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                         ws.offsets, (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
-    // log-depth reduction of continuation partials (a bucket can span up to segs segments)
-    for (int level = 0; ((size_t)1 << level) < segs; level++)
-      hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
-                         ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   }
   return hipGetLastError();
 }
 
-// Back half: summation by parts and the per-window sums, copied to host_out (W entries).
+// Front half of one multiexp: sort + accumulation, stream-ordered on st.
 template <class C>
-hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, typename C::P* host_out) {
+hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
+                     size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing) {
+  hipError_t e = msm_sort<C>(ws, st, d_scalars, n, d_idx, base_offset, sh);
+  if (e != hipSuccess) return e;
+  return msm_accumulate<C>(ws, st, d_bases, n, sh, timing);
+}
+
+// Back half: continuation fix-up, summation by parts and the per-window sums, copied to host_out (W entries).
+template <class C>
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out) {
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
+  // log-depth continuation fix-up: a bucket can span up to segs segments
+  const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
+  for (int level = 0; ((size_t)1 << level) < segs; level++)
+    hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
+                       ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
-  const size_t total = (size_t)sh.W * T;
+  const size_t total = (size_t)sh.Wb * T;
   hipLaunchKernelGGL(k_bucket_reduce<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
-                     ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, (uint32_t)sh.L, (uint32_t)sh.W,
+                     ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, (uint32_t)sh.L, (uint32_t)sh.Wb,
                      ws.seg_weighted, ws.seg_sum);
   hipLaunchKernelGGL(k_seg_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.seg_weighted, ws.seg_sum, T,
                      (uint32_t)sh.L, (uint32_t)total);
-  constexpr int TB = std::is_same<C, G1Ops>::value ? 128 : 64;
-  hipLaunchKernelGGL((k_tree_reduce<C, TB>), dim3(sh.W), dim3(TB), 0, st, ws.seg_weighted, T, ws.window_sums);
-  hipMemcpyAsync(host_out, ws.window_sums, sh.W * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+  // seg_weighted -> seg_sum -> seg_weighted ... -> window_sums
+  typename C::P* bufs[2] = {ws.seg_weighted, ws.seg_sum};
+  uint32_t Tin = T;
+  for (int lvl = 0;; lvl++) {
+    const uint32_t Tout = (Tin + 3) / 4;
+    typename C::P* dst = Tout == 1 ? ws.window_sums : bufs[(lvl + 1) & 1];
+    hipLaunchKernelGGL(k_sum_groups<C>, dim3(msm_blocks_for((size_t)sh.Wb * Tout, 64)), dim3(64), 0, st, bufs[lvl & 1],
+                       Tin, 4u, dst, Tout, (uint32_t)sh.Wb);
+    if (Tout == 1) break;
+    Tin = Tout;
+  }
+  hipMemcpyAsync(host_out, ws.window_sums, sh.Wb * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
   return hipGetLastError();
 }
 
@@ -355,7 +462,7 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
   if (e != hipSuccess) return e;
   e = ws.reserve_shape(n, sh);
   if (e != hipSuccess) return e;
-  return msm_back<C>(ws, st, sh, ws.host_window_sums);
+  return msm_back<C>(ws, st, n, sh, ws.host_window_sums);
 }
 
 }  // namespace bh

@@ -5,6 +5,7 @@
 #include <chrono>
 
 #include "api_internal.h"
+#include "crs.h"
 
 using namespace bh;
 
@@ -233,6 +234,58 @@ inline void shard_range(size_t n, size_t k, size_t N, size_t* lo, size_t* hi) {
 }
 
 // The 8 multiexps of create_proof (prover.rs:233-307) restricted to scalar shard
+// ---- SRS window tables.  A multiexp over a fixed base vector can trade HBM for work: with
+// T[i*W + w] = 2^(c*w) * P_i resident, every digit window adds into ONE set of 2^(c-1)
+// buckets, so the window size is no longer tied to W bucket reductions and c can grow
+// (c = 20 at 2^22 points: 13 instead of 16 additions per scalar).  Tables are built once
+// per (vector, c) -- a function of the CRS only, like Parameters::read -- and cost
+// n * ceil(256/c) points (5.2 GB for a 2^22-point G1 vector, 10.5 GB for b_g2).
+constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use plain windows
+
+int table_c_for(size_t used_per_shard) {
+  return used_per_shard >= TABLE_MIN_USED ? msm_table_c(used_per_shard) : 0;
+}
+
+bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c) {
+  if (c == 0 || srs->win_c == c) return BH_OK;
+  if (!srs->identity_idx.empty() || srs->n == 0) return BH_OK;  // identities: plain windows only
+  const int W = (256 + c - 1) / c;
+  if ((unsigned __int128)srs->n * W >= ((size_t)1 << 31)) return BH_OK;  // entry encoding limit
+  const bool g2 = srs->group == BH_G2;
+  const size_t pt_bytes = g2 ? 192 : 96;
+  const size_t bytes = srs->n * W * pt_bytes;
+  const size_t chunk = std::min<size_t>(srs->n, (size_t)1 << 19);
+  const size_t scratch = g2 ? window_table_scratch_bytes<G2Ops>(chunk, W) : window_table_scratch_bytes<G1Ops>(chunk, W);
+  srs->win.release();
+  srs->win_c = 0;
+  size_t free_b = 0, total_b = 0;
+  BH_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (bytes + scratch + ((size_t)4 << 30) > free_b) return BH_OK;  // keep 4 GB headroom
+  BH_TRY_HIP(srs->win.alloc(bytes));
+  DevBuf tmp;
+  BH_TRY_HIP(tmp.alloc(scratch));
+  const uint32_t* pts = srs->pts.as<uint32_t>();
+  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), tmp.p, chunk, ctx->stream));
+  else BH_TRY_HIP(window_table<G1Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), tmp.p, chunk, ctx->stream));
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  srs->win_c = c;
+  srs->win_W = W;
+  return BH_OK;
+}
+
+// the tables a proof of `w` on shard/nshards uses: h, l, a (aux part), b_g1, b_g2
+bh_status prepare_tables(bh_ctx* ctx, bh_params* params, size_t m, size_t na, size_t a_aux_used, size_t b_aux_used,
+                         size_t nshards) {
+  if (!ctx->tables || ctx->window_override) return BH_OK;
+  const size_t N = std::max<size_t>(nshards, 1);
+  bh_status s;
+  if ((s = ensure_table(ctx, &params->h, table_c_for((m - 1) / N)))) return s;
+  if ((s = ensure_table(ctx, &params->l, table_c_for(na / N)))) return s;
+  if ((s = ensure_table(ctx, &params->a, table_c_for(a_aux_used / N)))) return s;
+  if ((s = ensure_table(ctx, &params->b_g1, table_c_for(b_aux_used / N)))) return s;
+  return ensure_table(ctx, &params->b_g2, table_c_for(b_aux_used / N));
+}
+
 // `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
 // res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
 bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
@@ -249,6 +302,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(ctx->idx.alloc(maxn * 4));
   BH_TRY_HIP(ctx->dtmp.alloc((maxn / 64 + 2) * 4));
   BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(maxn / 64 + 2) * 4 + 64));
+
+  if ((s = prepare_tables(ctx, const_cast<bh_params*>(params), m, na, w->a_aux_total, w->b_aux_total, nshards)))
+    return s;
 
   // ---- error semantics (prover.rs:309-343 order: delta check, then the waits)
   const uint64_t* dens = w->dens.as<uint64_t>();
@@ -274,18 +330,29 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (s) return s;
     }
   }
-  // ---- H (prover.rs:210-234), device resident
-  hipEventRecord(ctx->ev[0], ctx->stream);
-  uint32_t* abc = ctx->staging.as<uint32_t>();
-  BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, ctx->stream));
-  if ((s = run_h_pipeline(ctx, D, abc))) return s;
-  // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
-  BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, ctx->stream));
-  hipEventRecord(ctx->ev[1], ctx->stream);
+  // Four streams, all ordered after whatever ran before on ctx->stream:
+  //   stream  (normal priority): the bucket accumulations back to back (VALU-bound critical path);
+  //   stream4 (normal): the H pipeline, filling the accumulations' ramp-down gaps;
+  //   stream3 (high):   density maps, then every multiexp's sort (memory-bound, runs ahead);
+  //   stream2 (high):   every multiexp's reduction tail as soon as it is accumulated.
+  // Each multiexp has its own workspace, so the only dependencies are the events below.
+  hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
+  hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated, [32] start
+  BH_TRY_HIP(hipEventRecord(jev[32], sA));
+  BH_TRY_HIP(hipStreamWaitEvent(sH, jev[32], 0));
+  BH_TRY_HIP(hipStreamWaitEvent(sS, jev[32], 0));
+  BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
 
-  // ---- the 8 multiexps (prover.rs:233-307), pipelined: job j's sort + accumulation
-  // run on stream A while job j-1's bucket reduction runs on stream B (ping-pong
-  // workspaces per curve); the host Horner-combines every job at the end.
+  // ---- H (prover.rs:210-234), device resident
+  hipEventRecord(ctx->ev[0], sH);
+  uint32_t* abc = ctx->staging.as<uint32_t>();
+  BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
+  if ((s = run_h_pipeline(ctx, D, abc, sH))) return s;
+  // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
+  BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, sH));
+  hipEventRecord(ctx->ev[1], sH);
+
+  // ---- the 8 multiexps (prover.rs:233-307)
   const uint32_t* inputs = w->inputs.as<uint32_t>();
   const uint32_t* aux = w->aux.as<uint32_t>();
   BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
@@ -293,87 +360,91 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   int32_t* idx_bin = idx_aaux + na;
   int32_t* idx_baux = idx_bin + ni;
   if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
-                                   ctx->dscan.as<uint32_t>(), ctx->stream));
-  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(),
-                                   ctx->stream));
+                                   ctx->dscan.as<uint32_t>(), sS));
+  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), sS));
   if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx_baux, ctx->dtmp.as<uint32_t>(),
-                                   ctx->dscan.as<uint32_t>(), ctx->stream));
+                                   ctx->dscan.as<uint32_t>(), sS));
   struct Job {
     bool g2;
     const bh_srs* srs;
-    size_t base_off;       // used when idx == nullptr
     const uint32_t* sc;
     size_t n;              // full query length (sharded below)
-    const int32_t* idx;
+    const int32_t* idx;    // density map (already offset into the base vector) or null
     size_t used;           // density-set scalars (roofline accounting)
     int out;               // result slot: G1 0..5 / G2 0..1
   };
-  // the big G2 job first so its (longest) tail hides under G1 accumulation
+  // G2 first (its accumulation hides the H pipeline), h after l so its sort finds H done
   const Job jobs[8] = {
-      {true, &params->b_g2, 0, aux, na, idx_baux, w->b_aux_total, 1},      // b_g2_aux
-      {false, &params->h, 0, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
-      {false, &params->l, 0, aux, na, nullptr, na, 1},                     // l
-      {false, &params->a, 0, aux, na, idx_aaux, w->a_aux_total, 3},        // a_aux
-      {false, &params->b_g1, 0, aux, na, idx_baux, w->b_aux_total, 5},     // b_g1_aux
-      {false, &params->a, 0, inputs, ni, nullptr, ni, 2},                  // a_inputs
-      {false, &params->b_g1, 0, inputs, ni, idx_bin, w->b_in_total, 4},    // b_g1_inputs
-      {true, &params->b_g2, 0, inputs, ni, idx_bin, w->b_in_total, 0},     // b_g2_inputs
+      {true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1},              // b_g2_aux
+      {false, &params->l, aux, na, nullptr, na, 1},                             // l
+      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
+      {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
+      {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
+      {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
+      {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
+      {true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0},             // b_g2_inputs
   };
-  MsmWorkspace<G1Ops>* ws1[2] = {&ctx->g1ws, &ctx->g1ws_b};
-  MsmWorkspace<G2Ops>* ws2[2] = {&ctx->g2ws, &ctx->g2ws_b};
-  hipEvent_t* back_done = ctx->jev + 40;  // [g1 slot0, g1 slot1, g2 slot0, g2 slot1]
-  bool used_slot[4] = {false, false, false, false};
-  int next1 = 0, next2 = 0;
   MsmShape shapes[8];
-  bool ran[8] = {false};
-  size_t lo, hi;
+  bool use_table[8] = {false};
+  size_t los[8], his[8];
+  for (int j = 0; j < 8; j++) {
+    shard_range(jobs[j].n, shard, nshards, &los[j], &his[j]);
+    if (his[j] == los[j]) continue;
+    const size_t used = (size_t)((unsigned __int128)jobs[j].used * (his[j] - los[j]) / std::max<size_t>(jobs[j].n, 1));
+    const bh_srs* srs = jobs[j].srs;
+    use_table[j] = srs->win_c && used >= TABLE_MIN_USED;
+    shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
+                             : msm_shape(his[j] - los[j], ctx->window_override);
+  }
+  // sorts, in accumulation order
   for (int j = 0; j < 8; j++) {
     const Job& J = jobs[j];
-    shard_range(J.n, shard, nshards, &lo, &hi);
-    if (hi <= lo) continue;
-    const size_t n = hi - lo;
-    const MsmShape sh = msm_shape(n, ctx->window_override);
-    shapes[j] = sh;
-    ran[j] = true;
-    const int slot = J.g2 ? next2 : next1;
-    const int ev_slot = (J.g2 ? 2 : 0) + slot;
-    if (used_slot[ev_slot]) BH_TRY_HIP(hipStreamWaitEvent(ctx->stream, back_done[ev_slot], 0));
-    MsmTiming tm;
-    tm.ev_acc_begin = ctx->jev[2 * j];
-    tm.ev_acc_end = ctx->jev[2 * j + 1];
-    const uint32_t* bases = J.srs->pts.as<uint32_t>();
-    const int32_t* ix = J.idx ? J.idx + lo : nullptr;
-    const uint32_t boff = (uint32_t)(J.base_off + lo);
-    if (J.g2) BH_TRY_HIP(msm_front<G2Ops>(*ws2[slot], ctx->stream, bases, J.sc + lo * 8, n, ix, boff, sh, &tm));
-    else BH_TRY_HIP(msm_front<G1Ops>(*ws1[slot], ctx->stream, bases, J.sc + lo * 8, n, ix, boff, sh, &tm));
-    BH_TRY_HIP(hipEventRecord(ctx->jev[16 + j], ctx->stream));
-    BH_TRY_HIP(hipStreamWaitEvent(ctx->stream2, ctx->jev[16 + j], 0));
-    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(*ws2[slot], ctx->stream2, sh, ctx->host_out2 + 128 * J.out));
-    else BH_TRY_HIP(msm_back<G1Ops>(*ws1[slot], ctx->stream2, sh, ctx->host_out1 + 128 * J.out));
-    BH_TRY_HIP(hipEventRecord(back_done[ev_slot], ctx->stream2));
-    used_slot[ev_slot] = true;
-    if (J.g2) next2 ^= 1;
-    else next1 ^= 1;
+    const size_t n = his[j] - los[j];
+    if (!n) continue;
+    if (J.sc == ctx->hbuf.as<uint32_t>()) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    const int32_t* ix = J.idx ? J.idx + los[j] : nullptr;
+    const uint32_t* sc = J.sc + los[j] * 8;
+    if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
+    else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
+    BH_TRY_HIP(hipEventRecord(jev[16 + j], sS));
   }
-  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
-  BH_TRY_HIP(hipStreamSynchronize(ctx->stream2));
+  // accumulations on the main stream, each tail on stream2 as soon as it is accumulated
+  for (int j = 0; j < 8; j++) {
+    const Job& J = jobs[j];
+    const size_t n = his[j] - los[j];
+    if (!n) continue;
+    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + j], 0));
+    MsmTiming tm;
+    tm.ev_acc_begin = jev[2 * j];
+    tm.ev_acc_end = jev[2 * j + 1];
+    const uint32_t* bases = use_table[j] ? J.srs->win.as<uint32_t>() : J.srs->pts.as<uint32_t>();
+    if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], sA, bases, n, shapes[j], &tm));
+    else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], sA, bases, n, shapes[j], &tm));
+    BH_TRY_HIP(hipEventRecord(jev[24 + j], sA));
+    BH_TRY_HIP(hipStreamWaitEvent(sT, jev[24 + j], 0));
+    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], sT, n, shapes[j], ctx->host_out2 + 128 * J.out));
+    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], sT, n, shapes[j], ctx->host_out1 + 128 * J.out));
+  }
+  BH_TRY_HIP(hipStreamSynchronize(sS));
+  BH_TRY_HIP(hipStreamSynchronize(sA));
+  BH_TRY_HIP(hipStreamSynchronize(sH));
+  BH_TRY_HIP(hipStreamSynchronize(sT));
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0;
   int g1_launches = 0, g2_launches = 0;
   for (int i = 0; i < 6; i++) res1[i] = jac_identity<Fp>();
   for (int i = 0; i < 2; i++) res2[i] = jac_identity<bh::Fp2>();
   for (int j = 0; j < 8; j++) {
-    if (!ran[j]) continue;
     const Job& J = jobs[j];
+    if (his[j] == los[j]) continue;
     float t = 0;
-    (void)hipEventElapsedTime(&t, ctx->jev[2 * j], ctx->jev[2 * j + 1]);
-    shard_range(J.n, shard, nshards, &lo, &hi);
-    const size_t pairs = (size_t)((unsigned __int128)J.used * (hi - lo) / std::max<size_t>(J.n, 1));
+    (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
+    const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
     if (J.g2) {
-      res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].W, shapes[j].c);
+      res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].Wb, shapes[j].c);
       g2_acc_ms += t; g2_launches++; g2_pairs += pairs;
     } else {
-      res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j].W, shapes[j].c);
+      res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j].Wb, shapes[j].c);
       g1_acc_ms += t; g1_launches++; g1_pairs += pairs;
     }
   }
@@ -432,6 +503,13 @@ constexpr size_t PARTIAL_BYTES = 6 * 96 + 2 * 192;
 }  // namespace
 
 extern "C" {
+
+bh_status bh_params_prepare(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t nshards) {
+  if (!ctx || !params || !w || nshards == 0) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  return prepare_tables(ctx, params, w->m, w->num_aux, w->a_aux_total, w->b_aux_total, nshards);
+}
 
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r_in[4],
                            const uint64_t s_in[4], uint8_t proof_out[192]) {

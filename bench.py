@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on a bounded sample (rank 0)")
     ap.add_argument("--cpu-log-constraints", type=int, default=16)
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
+    ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
     ap.add_argument("--exchange", default="rccl",
                     help="partial-sum exchange: rccl (library-driven RCCL all-gather over xGMI) or gloo (CPU rehearsal)")
     return ap.parse_args()
@@ -89,6 +90,12 @@ def main():
     t0 = time.time()
     witness = bh.Witness.chain(ctx, rounds)
     t_wit = time.time() - t0
+    t0 = time.time()
+    if args.tables:
+        params.prepare(witness, world)  # SRS window tables: a function of the CRS only
+    else:
+        ctx.set_tables(False)
+    t_tables = time.time() - t0
     r, s = 27134, 17146
     vk = params.vk_bytes()
     comm = None
@@ -190,8 +197,10 @@ def main():
         "breakdown_ms": {"h_pipeline": round(sum(t[1] for t in timings) / len(timings), 3),
                          "g1_accumulate": round(acc_ms / len(timings), 3),
                          "g2_accumulate": round(sum(t[5] for t in timings) / len(timings), 3),
+                         "g1_pairs": int(timings[-1][4]), "g2_pairs": int(timings[-1][7]),
                          "host_wall_prove": round(sum(t[0] for t in timings) / len(timings), 3)},
-        "setup_s": {"crs_generation": round(t_params, 2), "witness_synthesis_and_upload": round(t_wit, 2)},
+        "setup_s": {"crs_generation": round(t_params, 2), "witness_synthesis_and_upload": round(t_wit, 2),
+                    "srs_window_tables": round(t_tables, 2) if args.tables else None},
         "proof_sha_prefix": ref.hex()[:32] if ref else None,
     }
     print(json.dumps(out))

@@ -74,8 +74,14 @@ bh_status bh_ctx_destroy(bh_ctx* ctx);
 /* Pre-allocate workspaces for MSMs up to max_msm_len and domains up to 2^max_log_domain,
  * so that later calls allocate nothing. */
 bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domain);
-/* Force a window size for device MSMs (0 = automatic). Results never depend on it. */
+/* Force a window size for device MSMs (0 = automatic). Results never depend on it.
+ * A forced window also disables the prover's window tables. */
 bh_status bh_ctx_set_window(bh_ctx* ctx, int c);
+/* Prover SRS window tables (default 1 = on): for each large query of the Parameters the
+ * prover keeps T[i*W + w] = 2^(c*w) * P_i resident in HBM (built once per Parameters,
+ * ~31 GB at 2^22 constraints, skipped when HBM is short) so that all digit windows share
+ * one bucket set and c can grow.  Results never depend on it. */
+bh_status bh_ctx_set_tables(bh_ctx* ctx, int enable);
 
 /* ---- bases (Source over Arc<Vec<G1Affine|G2Affine>>) */
 bh_status bh_srs_upload(bh_ctx* ctx, int group, const uint8_t* uncompressed_be, size_t n, int checked,
@@ -127,6 +133,9 @@ bh_status bh_witness_upload(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, c
                             const uint64_t* aux_assignment, size_t num_aux, const uint64_t* a_aux_density,
                             const uint64_t* b_input_density, const uint64_t* b_aux_density, bh_witness** out);
 bh_status bh_witness_free(bh_witness* w);
+/* Build now (instead of inside the first proof) the window tables that proofs of witnesses
+ * shaped like w, split over nshards GPUs, will use.  Optional. */
+bh_status bh_params_prepare(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t nshards);
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r[4],
                            const uint64_t s[4], uint8_t proof_out[192]);
 

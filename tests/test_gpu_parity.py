@@ -250,3 +250,26 @@ def test_sharded_partials_combine(ctx, golden, nshards):
     w = bh.Witness.chain(ctx, 15)
     parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, nshards) for k in range(nshards))
     assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146).hex() == fx["proof"]
+
+
+@pytest.mark.parametrize("logc", [17, 20, 22])
+def test_window_tables_match_plain_windows(ctx, logc):
+    """SRS window tables (every digit window sharing one bucket set, larger c) give
+    byte-identical proofs to plain per-window buckets, on one device and sharded over
+    two (whose smaller shards pick a different c, so the tables are rebuilt).  At 2^22
+    (BASELINE.json configs[2]) this is the benchmark's own proof."""
+    bh = _bh()
+    rounds = (1 << (logc - 1)) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    ctx.set_tables(False)
+    try:
+        plain = bh.prove_witness(ctx, params, w, 27134, 17146)
+    finally:
+        ctx.set_tables(True)
+    params.prepare(w)
+    assert bh.prove_witness(ctx, params, w, 27134, 17146) == plain
+    parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, 2) for k in range(2))
+    assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
+    if logc == 22:
+        assert plain.hex().startswith("b320c6a265000d01babba804dc37ae10")
