@@ -245,27 +245,29 @@ static MsmTiming g_no_timing;
 bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
                         const int32_t* d_idx, Jac<Fp>* out, float* acc_ms) {
   if (n == 0) { *out = jac_identity<Fp>(); return BH_OK; }
-    MsmShape sh = msm_shape(n, ctx->window_override);
+  MsmShape sh = msm_shape(n, ctx->window_override);
+  fit_segments<G1Ops>(sh, n);
   MsmTiming tm;
   if (acc_ms) { tm.ev_acc_begin = ctx->ev[14]; tm.ev_acc_end = ctx->ev[15]; }
   BH_TRY_HIP(msm_window_sums<G1Ops>(ctx->g1ws, ctx->stream, bases->pts.as<uint32_t>(), d_scalars, n, d_idx,
                                     (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
-  *out = combine_g1(ctx->g1ws.host_window_sums, sh.W, sh.c);
+  *out = combine_g1(ctx->g1ws.host_window_sums, sh.Wb, sh.c);
   return BH_OK;
 }
 bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
                         const int32_t* d_idx, Jac<bh::Fp2>* out, float* acc_ms) {
   if (n == 0) { *out = jac_identity<bh::Fp2>(); return BH_OK; }
-    MsmShape sh = msm_shape(n, ctx->window_override);
+  MsmShape sh = msm_shape(n, ctx->window_override);
+  fit_segments<G2Ops>(sh, n);
   MsmTiming tm;
   if (acc_ms) { tm.ev_acc_begin = ctx->ev[14]; tm.ev_acc_end = ctx->ev[15]; }
   BH_TRY_HIP(msm_window_sums<G2Ops>(ctx->g2ws, ctx->stream, bases->pts.as<uint32_t>(), d_scalars, n, d_idx,
                                     (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
-  *out = combine_g2(ctx->g2ws.host_window_sums, sh.W, sh.c);
+  *out = combine_g2(ctx->g2ws.host_window_sums, sh.Wb, sh.c);
   return BH_OK;
 }
 

@@ -53,6 +53,9 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
 
 // The same MSM split in two stream-ordered halves: front = digit sort + bucket
 // accumulation, back = bucket reduction + window sums -> host_out (pinned, Wb entries).
+// set sh.S for curve C's accumulation kernel on the current device (see msm_impl.cuh)
+template <class C>
+void fit_segments(MsmShape& sh, size_t n);
 template <class C>
 hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
                     uint32_t base_offset, const MsmShape& sh);

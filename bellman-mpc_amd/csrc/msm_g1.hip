@@ -5,6 +5,7 @@ namespace bh {
 template struct MsmWorkspace<G1Ops>;
 template hipError_t msm_window_sums<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                          const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
+template void fit_segments<G1Ops>(MsmShape&, size_t);
 template hipError_t msm_sort<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, size_t, const int32_t*,
                                      uint32_t, const MsmShape&);
 template hipError_t msm_accumulate<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,

@@ -5,6 +5,7 @@ namespace bh {
 template struct MsmWorkspace<G2Ops>;
 template hipError_t msm_window_sums<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                          const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
+template void fit_segments<G2Ops>(MsmShape&, size_t);
 template hipError_t msm_sort<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const int32_t*,
                                      uint32_t, const MsmShape&);
 template hipError_t msm_accumulate<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,

@@ -261,6 +261,29 @@ inline int accumulate_variant() {
   return v;
 }
 
+// Segment length S so that the accumulation grid is exactly ROUNDS full waves of
+// resident workgroups (occupancy from the compiled kernel, CUs from the device): a
+// partial last round would leave most of the chip idle for its whole duration.
+template <class C>
+void fit_segments(MsmShape& sh, size_t n) {
+  static const size_t conc = [] {
+    int dev = 0, cus = 256, blocks = 1;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const void* k = accumulate_variant() ? (const void*)k_accumulate_pf<C> : (const void*)k_accumulate_dev<C>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
+    return (size_t)cus * (size_t)blocks * 256;
+  }();
+  static const size_t rounds = [] {
+    const char* e = getenv("BH_ACC_ROUNDS");
+    const int r = e ? atoi(e) : 4;
+    return (size_t)(r > 0 ? r : 4);
+  }();
+  const size_t E = n * (size_t)sh.W;
+  size_t S = (E + rounds * conc - 1) / (rounds * conc);
+  sh.S = (int)std::min<size_t>(std::max<size_t>(S, 8), (size_t)1 << 16);
+}
+
 template <class C>
 size_t MsmWorkspace<C>::bytes_needed(size_t n) {
   MsmShape sh = msm_shape(n, 0);

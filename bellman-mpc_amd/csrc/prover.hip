@@ -3,6 +3,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <cstdlib>
 
 #include "api_internal.h"
 #include "crs.h"
@@ -337,6 +338,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   //   stream2 (high):   every multiexp's reduction tail as soon as it is accumulated.
   // Each multiexp has its own workspace, so the only dependencies are the events below.
   hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
+  static const bool serial = [] {  // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
+    const char* e = getenv("BH_PROVER_SERIAL");
+    return e && e[0] == '1';
+  }();
+  if (serial) sT = sS = sH = sA;
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated, [32] start
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
   BH_TRY_HIP(hipStreamWaitEvent(sH, jev[32], 0));
@@ -395,6 +401,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     use_table[j] = srs->win_c && used >= TABLE_MIN_USED;
     shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
                              : msm_shape(his[j] - los[j], ctx->window_override);
+    if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
+    else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
   }
   // sorts, in accumulation order
   for (int j = 0; j < 8; j++) {
