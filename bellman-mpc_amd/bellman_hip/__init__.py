@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libbellman_hip.so")
+_LIB_PATH = os.environ.get("BH_LIB_OVERRIDE") or os.path.join(_HERE, "libbellman_hip.so")  # override: A/B builds
 
 R_MODULUS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 _MONT_R = pow(2, 256, R_MODULUS)

@@ -332,10 +332,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     }
   }
   // Four streams, all ordered after whatever ran before on ctx->stream:
-  //   stream  (normal priority): the bucket accumulations back to back (VALU-bound critical path);
-  //   stream4 (normal): the H pipeline, filling the accumulations' ramp-down gaps;
-  //   stream3 (high):   density maps, then every multiexp's sort (memory-bound, runs ahead);
-  //   stream2 (high):   every multiexp's reduction tail as soon as it is accumulated.
+  //   stream : the bucket accumulations back to back (VALU-bound critical path);
+  //   stream4: the H pipeline (after the first sort), then the G2 reduction tails;
+  //   stream3: density maps, then every multiexp's sort (memory-bound, runs ahead);
+  //   stream2: the G1 reduction tails, each as soon as its multiexp is accumulated.
   // Each multiexp has its own workspace, so the only dependencies are the events below.
   hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
   static const bool serial = [] {  // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
@@ -345,18 +345,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (serial) sT = sS = sH = sA;
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated, [32] start
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
-  BH_TRY_HIP(hipStreamWaitEvent(sH, jev[32], 0));
   BH_TRY_HIP(hipStreamWaitEvent(sS, jev[32], 0));
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
-
-  // ---- H (prover.rs:210-234), device resident
-  hipEventRecord(ctx->ev[0], sH);
-  uint32_t* abc = ctx->staging.as<uint32_t>();
-  BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
-  if ((s = run_h_pipeline(ctx, D, abc, sH))) return s;
-  // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
-  BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, sH));
-  hipEventRecord(ctx->ev[1], sH);
 
   // ---- the 8 multiexps (prover.rs:233-307)
   const uint32_t* inputs = w->inputs.as<uint32_t>();
@@ -404,18 +394,40 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
     else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
   }
+  // ---- H (prover.rs:210-234), device resident.  It starts once the first sort is done
+  // (so it does not delay the first accumulation) and is only needed by h's sort.
+  auto enqueue_h = [&](hipEvent_t after) -> bh_status {
+    BH_TRY_HIP(hipStreamWaitEvent(sH, after, 0));
+    hipEventRecord(ctx->ev[0], sH);
+    uint32_t* abc = ctx->staging.as<uint32_t>();
+    BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
+    bh_status hs = run_h_pipeline(ctx, D, abc, sH);
+    if (hs) return hs;
+    // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
+    BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, sH));
+    hipEventRecord(ctx->ev[1], sH);
+    return BH_OK;
+  };
+  bool h_enqueued = false;
+  hipEvent_t last_sorted = jev[32];
   // sorts, in accumulation order
   for (int j = 0; j < 8; j++) {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
     if (!n) continue;
-    if (J.sc == ctx->hbuf.as<uint32_t>()) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if (J.sc == ctx->hbuf.as<uint32_t>()) {
+      if ((s = enqueue_h(last_sorted))) return s;
+      h_enqueued = true;
+      BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    }
     const int32_t* ix = J.idx ? J.idx + los[j] : nullptr;
     const uint32_t* sc = J.sc + los[j] * 8;
     if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
     else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
     BH_TRY_HIP(hipEventRecord(jev[16 + j], sS));
+    if (last_sorted == jev[32]) last_sorted = jev[16 + j];
   }
+  if (!h_enqueued && (s = enqueue_h(last_sorted))) return s;  // keeps the H timing events valid
   // accumulations on the main stream, each tail on stream2 as soon as it is accumulated
   for (int j = 0; j < 8; j++) {
     const Job& J = jobs[j];
@@ -429,9 +441,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], sA, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], sA, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], sA));
-    BH_TRY_HIP(hipStreamWaitEvent(sT, jev[24 + j], 0));
-    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], sT, n, shapes[j], ctx->host_out2 + 128 * J.out));
-    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], sT, n, shapes[j], ctx->host_out1 + 128 * J.out));
+    // G2 tails on the H stream (idle by then), so that they never hold up the G1 tails
+    hipStream_t tail = J.g2 ? sH : sT;
+    BH_TRY_HIP(hipStreamWaitEvent(tail, jev[24 + j], 0));
+    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], tail, n, shapes[j], ctx->host_out2 + 128 * J.out));
+    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], tail, n, shapes[j], ctx->host_out1 + 128 * J.out));
   }
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
