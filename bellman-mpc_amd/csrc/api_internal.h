@@ -72,7 +72,7 @@ struct bh_srs {
   // prover window table (built lazily, see prepare_tables in prover.hip):
   // win[i*win_W + w] = 2^(win_c*w) * P_i, packed affine
   bh::DevBuf win;
-  int win_c = 0, win_W = 0;
+  int win_c = 0, win_W = 0, win_rec = 0;  // win_rec: u32 words per record (128-B aligned)
 };
 
 struct bh_params {

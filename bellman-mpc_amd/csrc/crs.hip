@@ -85,7 +85,7 @@ struct Inv<Fp2Ops> {
 // one thread per CHUNK consecutive points; prefix products kept in `scratch`
 template <class C, int CHUNK>
 __global__ void __launch_bounds__(64) k_normalize(const typename C::P* pts, size_t n, typename FieldOf<C>::F::T* scratch,
-                                                  uint32_t* out_packed) {
+                                                  uint32_t* out_packed, uint32_t rec) {
   using F = typename FieldOf<C>::F;
   using T = typename F::T;
   constexpr int PW = F::PACKED_WORDS;
@@ -109,8 +109,8 @@ __global__ void __launch_bounds__(64) k_normalize(const typename C::P* pts, size
     // 1/ZZ = ZZZ / z ; 1/ZZZ = ZZ / z
     const T x = F::reduce(F::mul(p.X, F::mul(p.ZZZ, zinv)));
     const T y = F::reduce(F::mul(p.Y, F::mul(p.ZZ, zinv)));
-    F::pack(x, out_packed + i * 2 * PW);
-    F::pack(y, out_packed + i * 2 * PW + PW);
+    F::pack(x, out_packed + i * rec);
+    F::pack(y, out_packed + i * rec + PW);
   }
 }
 
@@ -125,7 +125,8 @@ hipError_t fixed_base_batch(const uint32_t* d_table, const uint32_t* d_scalars, 
   const size_t threads = (n + CHUNK - 1) / CHUNK;
   hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st,
                      reinterpret_cast<const P*>(d_xyzz), n,
-                     reinterpret_cast<typename FieldOf<C>::F::T*>(d_scratch), d_out);
+                     reinterpret_cast<typename FieldOf<C>::F::T*>(d_scratch), d_out,
+                     (uint32_t)(2 * FieldOf<C>::F::PACKED_WORDS));
   return hipGetLastError();
 }
 
@@ -149,8 +150,8 @@ size_t window_table_scratch_bytes(size_t chunk, int W) {
 }
 
 template <class C>
-hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t* d_out, void* d_scratch,
-                        size_t chunk, hipStream_t st) {
+hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t* d_out, uint32_t rec,
+                        void* d_scratch, size_t chunk, hipStream_t st) {
   using P = typename C::P;
   using T = typename FieldOf<C>::F::T;
   constexpr int PW = FieldOf<C>::F::PACKED_WORDS;
@@ -164,7 +165,7 @@ hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t*
     const size_t m = cnt * (size_t)W;
     const size_t threads = (m + CHUNK - 1) / CHUNK;
     hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, xyzz, m,
-                       prefix, d_out + i0 * (size_t)W * 2 * PW);
+                       prefix, d_out + i0 * (size_t)W * rec, rec);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -173,8 +174,10 @@ hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t*
 
 template size_t window_table_scratch_bytes<G1Ops>(size_t, int);
 template size_t window_table_scratch_bytes<G2Ops>(size_t, int);
-template hipError_t window_table<G1Ops>(const uint32_t*, size_t, int, int, uint32_t*, void*, size_t, hipStream_t);
-template hipError_t window_table<G2Ops>(const uint32_t*, size_t, int, int, uint32_t*, void*, size_t, hipStream_t);
+template hipError_t window_table<G1Ops>(const uint32_t*, size_t, int, int, uint32_t*, uint32_t, void*, size_t,
+                                        hipStream_t);
+template hipError_t window_table<G2Ops>(const uint32_t*, size_t, int, int, uint32_t*, uint32_t, void*, size_t,
+                                        hipStream_t);
 
 template hipError_t fixed_base_batch<G1Ops>(const uint32_t*, const uint32_t*, size_t, void*, void*, uint32_t*,
                                             hipStream_t);

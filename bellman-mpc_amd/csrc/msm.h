@@ -15,6 +15,7 @@ struct MsmShape {
   int S;    // sorted entries per accumulation thread
   int Wb;   // bucket windows: W, or 1 with a window table (all windows share the buckets)
   int pre;  // 1: bases are a window table T[i*W + w] = 2^(c*w) * P_i (entry = i*W + w)
+  int rec;  // u32 words per base record (0: packed affine, 2 x PACKED_WORDS)
 };
 MsmShape msm_shape(size_t n, int c_override);
 // shape for a window table: c from the cost model n*ceil(256/c) + ~6.5 * 2^(c-1)

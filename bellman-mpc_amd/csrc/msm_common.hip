@@ -201,6 +201,7 @@ MsmShape msm_shape(size_t n, int c_override) {
   sh.S = S;
   sh.Wb = sh.W;
   sh.pre = 0;
+  sh.rec = 0;
   return sh;
 }
 

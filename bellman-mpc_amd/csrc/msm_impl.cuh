@@ -12,11 +12,11 @@ static inline unsigned msm_blocks_for(size_t n, unsigned bs) { return (unsigned)
 
 // ----------------------------------------------------------------- accumulate
 template <class C>
-__device__ __forceinline__ typename C::A load_base(const uint32_t* bases, uint32_t e) {
+__device__ __forceinline__ typename C::A load_base(const uint32_t* bases, uint32_t e, uint32_t rec) {
   using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
   constexpr int PW = F::PACKED_WORDS;
   const uint32_t idx = e & 0x7fffffffu;
-  const uint4* p = reinterpret_cast<const uint4*>(bases + (size_t)idx * 2 * PW);
+  const uint4* p = reinterpret_cast<const uint4*>(bases + (size_t)idx * rec);
   uint32_t w[2 * PW];
 #pragma unroll
   for (int k = 0; k < PW / 2; k++) {
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(64) k_sum_groups(const typename C::P* in, uint
 // The accumulate kernel needs E; it reads it from offsets[nbt] on device.
 template <class C>
 __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
-                                                        const uint32_t* bases, uint32_t S,
+                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
                                                         typename C::P* bucket_sums, typename C::P* conts,
                                                         uint32_t* cont_bucket) {
   const uint32_t E = offsets[nbt];
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries,
       started_here = true;
       acc = C::identity();
     }
-    const typename C::A a = load_base<C>(bases, entries[j]);
+    const typename C::A a = load_base<C>(bases, entries[j], rec);
     acc = C::madd(acc, a);
   }
   if (started_here) store_point<C>(&bucket_sums[b], acc);
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries,
 // owns NQ x 64 x 16 B of LDS, lane l's base occupying slot l of each of the NQ rows.
 template <class C>
 __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
-                                                       const uint32_t* bases, uint32_t S,
+                                                       const uint32_t* bases, uint32_t rec, uint32_t S,
                                                        typename C::P* bucket_sums, typename C::P* conts,
                                                        uint32_t* cont_bucket) {
   using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, 
   const uint32_t end = min(pos0 + S, E);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   auto issue = [&](uint32_t e) {
-    const uint32_t* src = bases + (size_t)(e & 0x7fffffffu) * 2 * PW;
+    const uint32_t* src = bases + (size_t)(e & 0x7fffffffu) * rec;
 #pragma unroll
     for (int q = 0; q < NQ; q++)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
@@ -426,12 +426,16 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     const size_t Emax = n * (size_t)sh.W;
     const size_t segs = (Emax + sh.S - 1) / sh.S;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
+    using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+    const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
     if (accumulate_variant())
       hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
+                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
+                         ws.cont_bucket);
     else
       hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, (uint32_t)nbt, d_bases, (uint32_t)sh.S, ws.bucket_sums, ws.conts, ws.cont_bucket);
+                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
+                         ws.cont_bucket);
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
   }
   return hipGetLastError();

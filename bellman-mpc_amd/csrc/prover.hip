@@ -240,7 +240,8 @@ inline void shard_range(size_t n, size_t k, size_t N, size_t* lo, size_t* hi) {
 // buckets, so the window size is no longer tied to W bucket reductions and c can grow
 // (c = 20 at 2^22 points: 13 instead of 16 additions per scalar).  Tables are built once
 // per (vector, c) -- a function of the CRS only, like Parameters::read -- and cost
-// n * ceil(256/c) points (5.2 GB for a 2^22-point G1 vector, 10.5 GB for b_g2).
+// n * ceil(256/c) points, each padded to whole 128-byte lines so one gather is one (G1)
+// or two (G2) lines (7 GB for a 2^22-point G1 vector at c = 20, 14 GB for b_g2).
 constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use plain windows
 
 int table_c_for(size_t used_per_shard) {
@@ -253,8 +254,8 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c) {
   const int W = (256 + c - 1) / c;
   if ((unsigned __int128)srs->n * W >= ((size_t)1 << 31)) return BH_OK;  // entry encoding limit
   const bool g2 = srs->group == BH_G2;
-  const size_t pt_bytes = g2 ? 192 : 96;
-  const size_t bytes = srs->n * W * pt_bytes;
+  const uint32_t rec = g2 ? 64 : 32;  // 96 / 192-byte points padded to whole 128-byte lines
+  const size_t bytes = srs->n * W * rec * 4;
   const size_t chunk = std::min<size_t>(srs->n, (size_t)1 << 19);
   const size_t scratch = g2 ? window_table_scratch_bytes<G2Ops>(chunk, W) : window_table_scratch_bytes<G1Ops>(chunk, W);
   srs->win.release();
@@ -266,11 +267,12 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c) {
   DevBuf tmp;
   BH_TRY_HIP(tmp.alloc(scratch));
   const uint32_t* pts = srs->pts.as<uint32_t>();
-  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), tmp.p, chunk, ctx->stream));
-  else BH_TRY_HIP(window_table<G1Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), tmp.p, chunk, ctx->stream));
+  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
+  else BH_TRY_HIP(window_table<G1Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   srs->win_c = c;
   srs->win_W = W;
+  srs->win_rec = (int)rec;
   return BH_OK;
 }
 
@@ -391,6 +393,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     use_table[j] = srs->win_c && used >= TABLE_MIN_USED;
     shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
                              : msm_shape(his[j] - los[j], ctx->window_override);
+    if (use_table[j]) shapes[j].rec = srs->win_rec;
     if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
     else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
   }
