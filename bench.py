@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point, scalar)
 G2_PAIR_BYTES = 224
+TRAFFIC_FILE = "r01_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
 
 
 def parse():
@@ -165,16 +166,25 @@ def main():
         return
     ms = elapsed * 1000.0 / args.steps
     value = n_constraints * args.steps / elapsed
-    # dominant kernel: G1 bucket accumulation (k_accumulate_dev<G1>), device events
+    # dominant kernel: G1 bucket accumulation (k_accumulate_pf<G1>), device events around every
+    # launch of the timed steps; algorithmic bytes = 128 B per (base, scalar) pair
     acc_ms = sum(t[2] for t in timings)
     launches = sum(t[3] for t in timings)
     pairs = sum(t[4] for t in timings)
     achieved = (pairs * G1_PAIR_BYTES / 1e9) / (acc_ms / 1e3) if acc_ms > 0 else None
-    roof = {"bound": "hbm", "kernel": "k_accumulate_dev<G1>",
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", TRAFFIC_FILE)
+    if os.path.exists(tpath) and k == 22:
+        with open(tpath) as f:
+            traffic = round(json.load(f)["traffic_bytes_per_launch"])
+        traffic_src = f"profiles/{TRAFFIC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+    roof = {"bound": "hbm", "kernel": "k_accumulate_pf<G1>",
             "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
+            "traffic_source": traffic_src,
             "avg_launch_ms": round(acc_ms / launches, 4) if launches else None,
-            "algorithmic_bytes_per_launch": round(pairs * G1_PAIR_BYTES / launches) if launches else None}
+            "algorithmic_bytes_per_launch": round(pairs * G1_PAIR_BYTES / launches) if launches else None,
+            "note": "VALU-bound (XYZZ mixed additions on 29-bit limbs): see DESIGN.md section 4"}
     base = cpu_baseline(bh, ctx, args.cpu_log_constraints, None) if args.cpu_baseline else None
     out = {
         "metric": "Groth16 constraints/sec, BLS12-381, 2^22-constraint R1CS",
