@@ -243,6 +243,7 @@ inline void shard_range(size_t n, size_t k, size_t N, size_t* lo, size_t* hi) {
 // n * ceil(256/c) points, each padded to whole 128-byte lines so one gather is one (G1)
 // or two (G2) lines (7 GB for a 2^22-point G1 vector at c = 20, 14 GB for b_g2).
 constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use plain windows
+constexpr size_t SMALL_JOB = 4096;                   // run whole on a side stream (latency-bound)
 
 int table_c_for(size_t used_per_shard) {
   return used_per_shard >= TABLE_MIN_USED ? msm_table_c(used_per_shard) : 0;
@@ -335,7 +336,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   // Four streams, all ordered after whatever ran before on ctx->stream:
   //   stream : the bucket accumulations back to back (VALU-bound critical path);
-  //   stream4: the H pipeline (after the first sort), then the G2 reduction tails;
+  //   stream4: the small (public-input) multiexps, the H pipeline (after the first
+  //            accumulation), then the G2 reduction tails;
   //   stream3: density maps, then every multiexp's sort (memory-bound, runs ahead);
   //   stream2: the G1 reduction tails, each as soon as its multiexp is accumulated.
   // Each multiexp has its own workspace, so the only dependencies are the events below.
@@ -345,7 +347,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     return e && e[0] == '1';
   }();
   if (serial) sT = sS = sH = sA;
-  hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated, [32] start
+  hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated,
+                               // [32] start, [33] density maps ready
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
   BH_TRY_HIP(hipStreamWaitEvent(sS, jev[32], 0));
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
@@ -371,12 +374,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     size_t used;           // density-set scalars (roofline accounting)
     int out;               // result slot: G1 0..5 / G2 0..1
   };
-  // G2 first (its accumulation hides the H pipeline), h after l so its sort finds H done
+  // G2 first (the longest tail gets the most overlap), h fourth so H has two
+  // accumulations of slack
   const Job jobs[8] = {
       {true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1},              // b_g2_aux
       {false, &params->l, aux, na, nullptr, na, 1},                             // l
-      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
       {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
+      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
       {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
       {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
       {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
@@ -411,44 +415,76 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     hipEventRecord(ctx->ev[1], sH);
     return BH_OK;
   };
-  bool h_enqueued = false;
-  hipEvent_t last_sorted = jev[32];
-  // sorts, in accumulation order
-  for (int j = 0; j < 8; j++) {
+  auto sort_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
-    if (!n) continue;
-    if (J.sc == ctx->hbuf.as<uint32_t>()) {
-      if ((s = enqueue_h(last_sorted))) return s;
-      h_enqueued = true;
-      BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    }
     const int32_t* ix = J.idx ? J.idx + los[j] : nullptr;
     const uint32_t* sc = J.sc + los[j] * 8;
-    if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
-    else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], sS, sc, n, ix, (uint32_t)los[j], shapes[j]));
-    BH_TRY_HIP(hipEventRecord(jev[16 + j], sS));
-    if (last_sorted == jev[32]) last_sorted = jev[16 + j];
-  }
-  if (!h_enqueued && (s = enqueue_h(last_sorted))) return s;  // keeps the H timing events valid
-  // accumulations on the main stream, each tail on stream2 as soon as it is accumulated
-  for (int j = 0; j < 8; j++) {
+    if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
+    else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
+    BH_TRY_HIP(hipEventRecord(jev[16 + j], st));
+    return BH_OK;
+  };
+  auto acc_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
-    if (!n) continue;
-    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + j], 0));
+    BH_TRY_HIP(hipStreamWaitEvent(st, jev[16 + j], 0));
     MsmTiming tm;
     tm.ev_acc_begin = jev[2 * j];
     tm.ev_acc_end = jev[2 * j + 1];
     const uint32_t* bases = use_table[j] ? J.srs->win.as<uint32_t>() : J.srs->pts.as<uint32_t>();
-    if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], sA, bases, n, shapes[j], &tm));
-    else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], sA, bases, n, shapes[j], &tm));
-    BH_TRY_HIP(hipEventRecord(jev[24 + j], sA));
-    // G2 tails on the H stream (idle by then), so that they never hold up the G1 tails
-    hipStream_t tail = J.g2 ? sH : sT;
-    BH_TRY_HIP(hipStreamWaitEvent(tail, jev[24 + j], 0));
-    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], tail, n, shapes[j], ctx->host_out2 + 128 * J.out));
-    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], tail, n, shapes[j], ctx->host_out1 + 128 * J.out));
+    if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
+    else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
+    BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
+    return BH_OK;
+  };
+  auto tail_job = [&](int j, hipStream_t st) -> bh_status {
+    const Job& J = jobs[j];
+    const size_t n = his[j] - los[j];
+    BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + j], 0));
+    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out));
+    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out));
+    return BH_OK;
+  };
+  // Small multiexps (the public-input queries) are latency-bound: run them whole on the
+  // H stream first, inside the start-up gap, after the density maps.
+  BH_TRY_HIP(hipEventRecord(jev[33], sS));
+  BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
+  int big[8], nbig = 0;
+  for (int j = 0; j < 8; j++) {
+    const size_t n = his[j] - los[j];
+    if (!n) continue;
+    if (n < SMALL_JOB && jobs[j].sc != ctx->hbuf.as<uint32_t>()) {
+      if ((s = sort_job(j, sH)) || (s = acc_job(j, sH)) || (s = tail_job(j, sH))) return s;
+    } else {
+      big[nbig++] = j;
+    }
+  }
+  // Large ones: sorts run ahead on stream3, accumulations back to back on the main stream,
+  // each tail on a side stream (G2 tails on the H stream, so they never hold up G1 tails).
+  // H starts once the first accumulation is done -- earlier it keeps CUs from the first,
+  // whole-CU G2 accumulation -- and is needed only by h's sort, two accumulations later.
+  int h_pos = nbig;
+  for (int q = 0; q < nbig; q++)
+    if (jobs[big[q]].sc == ctx->hbuf.as<uint32_t>()) h_pos = q;
+  for (int q = 0; q < h_pos; q++)
+    if ((s = sort_job(big[q], sS))) return s;
+  int next_acc = 0;
+  if (h_pos > 0) {
+    if ((s = acc_job(big[0], sA))) return s;
+    if ((s = enqueue_h(jev[24 + big[0]]))) return s;  // ahead of the first tail on its stream
+    if ((s = tail_job(big[0], jobs[big[0]].g2 ? sH : sT))) return s;
+    next_acc = 1;
+  } else if ((s = enqueue_h(jev[33]))) {
+    return s;
+  }
+  for (int q = h_pos; q < nbig; q++) {
+    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if ((s = sort_job(big[q], sS))) return s;
+  }
+  for (int q = next_acc; q < nbig; q++) {
+    const int j = big[q];
+    if ((s = acc_job(j, sA)) || (s = tail_job(j, jobs[j].g2 ? sH : sT))) return s;
   }
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
