@@ -216,7 +216,8 @@ class Context:
         _check(_lib.bh_ctx_synchronize(self.h))
 
     def last_timings(self):
-        out = (ctypes.c_double * 8)()
+        """bh_last_timings: see include/bellman_hip.h for the 10 fields."""
+        out = (ctypes.c_double * 10)()
         _check(_lib.bh_last_timings(self.h, out))
         return list(out)
 

@@ -97,6 +97,34 @@ __global__ void __launch_bounds__(256) k_points_to_dev(uint32_t* pts, size_t n, 
   }
 }
 
+// Prime-order subgroup check of Parameters::read(checked) (G1Affine/G2Affine::
+// from_uncompressed reject points that are not torsion-free): [r]P == O by a
+// double-and-add over the bits of r in XYZZ coordinates.  Runs on the device-form points.
+template <bool G2>
+__global__ void __launch_bounds__(256) k_subgroup_check(const uint32_t* pts, size_t n, uint32_t* bad) {
+  using C = typename std::conditional<G2, G2Ops, G1Ops>::type;
+  using F = typename std::conditional<G2, Fp2Ops, FpOps>::type;
+  constexpr int PW = F::PACKED_WORDS;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* p = pts + i * 2 * PW;
+  uint32_t nz = 0;
+  for (int k = 0; k < 2 * PW; k++) nz |= p[k];
+  if (!nz) return;  // the identity encoding
+  typename C::A a;
+  a.x = F::unpack(p);
+  a.y = F::unpack(p + PW);
+  // r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001, LE words
+  constexpr uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                             0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  typename C::P acc = C::from_affine(a);
+  for (int bit = 253; bit >= 0; bit--) {  // bit 254 is the leading one
+    acc = C::dbl(acc);
+    if ((R[bit >> 5] >> (bit & 31)) & 1u) acc = C::madd(acc, a);
+  }
+  if (!C::is_identity(acc)) atomicOr(bad, 2u);
+}
+
 // ------------------------------------------------------------------ SRS
 // host affine points -> device (packed canonical words, then device conversion)
 bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_pts, size_t n, bh_srs* out) {
@@ -193,10 +221,20 @@ bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n,
       hipLaunchKernelGGL(k_points_to_dev<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
                          checked, bad.as<uint32_t>());
     BH_TRY_HIP(hipGetLastError());
+    if (checked) {
+      if (group == BH_G1)
+        hipLaunchKernelGGL(k_subgroup_check<false>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(),
+                           n, bad.as<uint32_t>());
+      else
+        hipLaunchKernelGGL(k_subgroup_check<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(),
+                           n, bad.as<uint32_t>());
+      BH_TRY_HIP(hipGetLastError());
+    }
     uint32_t hbad = 0;
     BH_TRY_HIP(hipMemcpyAsync(&hbad, bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
     BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
-    if (hbad) return BH_ERR_NOT_ON_CURVE;
+    if (hbad & 1u) return BH_ERR_NOT_ON_CURVE;
+    if (hbad & 2u) return BH_ERR_NOT_IN_SUBGROUP;
   }
   return BH_OK;
 }
@@ -502,6 +540,7 @@ const char* bh_status_string(bh_status s) {
     case BH_ERR_UNCONSTRAINED_VARIABLE: return "auxiliary variable was unconstrained";
     case BH_ERR_INVALID_ARGUMENT: return "invalid argument";
     case BH_ERR_INVALID_ENCODING: return "invalid point encoding";
+    case BH_ERR_NOT_IN_SUBGROUP: return "point is not in the prime-order subgroup";
     case BH_ERR_NOT_ON_CURVE: return "point not on curve";
     case BH_ERR_OUT_OF_MEMORY: return "device out of memory";
     case BH_ERR_HIP: return "HIP runtime error";
@@ -534,7 +573,8 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   for (auto& e : c->jev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
   if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->host_counts, 16 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     delete c;
     return BH_ERR_OUT_OF_MEMORY;
   }
@@ -558,6 +598,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   for (auto& e : ctx->jev) if (e) (void)hipEventDestroy(e);
   if (ctx->host_out1) (void)hipHostFree(ctx->host_out1);
   if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
+  if (ctx->host_counts) (void)hipHostFree(ctx->host_counts);
   (void)hipStreamDestroy(ctx->stream);
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);

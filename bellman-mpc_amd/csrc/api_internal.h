@@ -122,7 +122,8 @@ struct bh_ctx {
   bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
-  double last_timings[8] = {};
+  double last_timings[10] = {};
+  uint32_t* host_counts = nullptr;  // pinned: entries (= mixed additions) of each prover multiexp
   std::mutex mu;
 };
 

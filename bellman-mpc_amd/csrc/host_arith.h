@@ -419,9 +419,19 @@ static inline bool on_curve(const AffinePt<T>& a) {
   return sqr(a.y) == add(mul(sqr(a.x), a.x), CurveB<T>::b());
 }
 
-// G1Affine::from_uncompressed_unchecked semantics (+ on-curve check when checked);
-// returns 0 ok, -1 invalid encoding, -2 not on curve
-static inline int g1_from_uncompressed(const uint8_t* in96, AffinePt<Fp>* out, bool check_curve) {
+// [r]P == O (torsion-freeness, part of G1Affine/G2Affine::from_uncompressed)
+template <class T>
+static inline bool in_subgroup(const AffinePt<T>& p) {
+  static const uint64_t R[4] = {0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull,
+                                0x73eda753299d7d48ull};
+  return p.infinity || jac_is_identity(jac_mul(jac_from_affine(p), R, 4));
+}
+
+// G1Affine::from_uncompressed_unchecked semantics (+ on-curve check when check_curve,
+// + subgroup check when check_subgroup); returns 0 ok, -1 invalid encoding, -2 not on
+// curve, -3 not in the subgroup
+static inline int g1_from_uncompressed(const uint8_t* in96, AffinePt<Fp>* out, bool check_curve,
+                                       bool check_subgroup = false) {
   uint8_t flags = in96[0] >> 5;
   if (flags & 0x4) return -1;  // compression flag set
   if (flags & 0x1) return -1;  // sort flag set
@@ -437,9 +447,11 @@ static inline int g1_from_uncompressed(const uint8_t* in96, AffinePt<Fp>* out, b
   if (!fp_from_be(in96 + 48, &out->y)) return -1;
   out->infinity = false;
   if (check_curve && !on_curve(*out)) return -2;
+  if (check_subgroup && !in_subgroup(*out)) return -3;
   return 0;
 }
-static inline int g2_from_uncompressed(const uint8_t* in192, AffinePt<Fp2>* out, bool check_curve) {
+static inline int g2_from_uncompressed(const uint8_t* in192, AffinePt<Fp2>* out, bool check_curve,
+                                       bool check_subgroup = false) {
   uint8_t flags = in192[0] >> 5;
   if (flags & 0x4) return -1;
   if (flags & 0x1) return -1;
@@ -457,6 +469,7 @@ static inline int g2_from_uncompressed(const uint8_t* in192, AffinePt<Fp2>* out,
   if (!fp_from_be(in192 + 144, &out->y.c0)) return -1;
   out->infinity = false;
   if (check_curve && !on_curve(*out)) return -2;
+  if (check_subgroup && !in_subgroup(*out)) return -3;
   return 0;
 }
 

@@ -33,14 +33,14 @@ struct Reader {
 bh_status read_g1_vk(Reader& r, AffinePt<Fp>* out, bool reject_identity) {
   const uint8_t* b;
   if (!r.take(96, &b)) return BH_ERR_INVALID_ENCODING;
-  if (g1_from_uncompressed(b, out, true) != 0) return BH_ERR_INVALID_ENCODING;
+  if (g1_from_uncompressed(b, out, true, true) != 0) return BH_ERR_INVALID_ENCODING;
   if (reject_identity && out->infinity) return BH_ERR_INVALID_ENCODING;
   return BH_OK;
 }
 bh_status read_g2_vk(Reader& r, AffinePt<bh::Fp2>* out) {
   const uint8_t* b;
   if (!r.take(192, &b)) return BH_ERR_INVALID_ENCODING;
-  if (g2_from_uncompressed(b, out, true) != 0) return BH_ERR_INVALID_ENCODING;
+  if (g2_from_uncompressed(b, out, true, true) != 0) return BH_ERR_INVALID_ENCODING;
   return BH_OK;
 }
 
@@ -436,6 +436,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
+    // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
+    const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
+    BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
+                              hipMemcpyDeviceToHost, st));
     return BH_OK;
   };
   auto tail_job = [&](int j, hipStream_t st) -> bh_status {
@@ -491,7 +495,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(hipStreamSynchronize(sH));
   BH_TRY_HIP(hipStreamSynchronize(sT));
   float g1_acc_ms = 0, g2_acc_ms = 0;
-  size_t g1_pairs = 0, g2_pairs = 0;
+  size_t g1_pairs = 0, g2_pairs = 0, g1_adds = 0, g2_adds = 0;
   int g1_launches = 0, g2_launches = 0;
   for (int i = 0; i < 6; i++) res1[i] = jac_identity<Fp>();
   for (int i = 0; i < 2; i++) res2[i] = jac_identity<bh::Fp2>();
@@ -503,10 +507,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
     if (J.g2) {
       res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].Wb, shapes[j].c);
-      g2_acc_ms += t; g2_launches++; g2_pairs += pairs;
+      g2_acc_ms += t; g2_launches++; g2_pairs += pairs; g2_adds += ctx->host_counts[j];
     } else {
       res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j].Wb, shapes[j].c);
-      g1_acc_ms += t; g1_launches++; g1_pairs += pairs;
+      g1_acc_ms += t; g1_launches++; g1_pairs += pairs; g1_adds += ctx->host_counts[j];
     }
   }
 
@@ -521,6 +525,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ctx->last_timings[5] = g2_acc_ms;
   ctx->last_timings[6] = g2_launches;
   ctx->last_timings[7] = (double)g2_pairs;
+  ctx->last_timings[8] = (double)g1_adds;
+  ctx->last_timings[9] = (double)g2_adds;
   return BH_OK;
 }
 
@@ -632,6 +638,8 @@ bh_status bh_proof_from_partials(const uint8_t* vk_bytes, size_t vk_len, const u
                                  const uint64_t r[4], const uint64_t s[4], uint8_t proof_out[192]) {
   if (!vk_bytes || !partials || !nshards || !r || !s || !proof_out) return BH_ERR_INVALID_ARGUMENT;
   if (vk_len < 96 * 3 + 192 * 3) return BH_ERR_INVALID_ENCODING;
+  // on-curve checks only: the VK comes from bh_vk_write of loaded (checked) Parameters and
+  // the partials are sums of subgroup points; this runs once per multi-GPU proof
   VkHost vk;
   AffinePt<bh::Fp2> gamma;
   const uint8_t* p = vk_bytes;
@@ -676,7 +684,7 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
   return st;
 }
 
-bh_status bh_last_timings(const bh_ctx* ctx, double out[8]) {
+bh_status bh_last_timings(const bh_ctx* ctx, double out[10]) {
   if (!ctx || !out) return BH_ERR_INVALID_ARGUMENT;
   memcpy(out, ctx->last_timings, sizeof ctx->last_timings);
   return BH_OK;

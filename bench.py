@@ -28,7 +28,10 @@ sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point, scalar)
 G2_PAIR_BYTES = 224
-TRAFFIC_FILE = "r01_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
+TRAFFIC_FILE = "r01_pmc_traffic_accumulate_g1.json"
+G1_MADD_PEAK = 6.51            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X
+MADS_PER_G1_MADD = 8 * 391 + 2 * 300
+MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X  # tools/pmc_traffic.py output for the 2^22 workload
 
 
 def parse():
@@ -39,6 +42,7 @@ def parse():
     ap.add_argument("--log-constraints", type=int, default=22)
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on a bounded sample (rank 0)")
     ap.add_argument("--cpu-log-constraints", type=int, default=16)
+    ap.add_argument("--cpu-1t-log-constraints", type=int, default=12, help="1-thread CPU sample (0: skip)")
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
     ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
     ap.add_argument("--exchange", default="rccl",
@@ -46,10 +50,22 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(bh, ctx, log_c, gpu_params_cache):
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(bh, ctx, log_c, log_c_1t):
     """bench leg only: the oracle's C++ port of bellman's multicore prover core
     (oracle/cpu/bellman_port.cpp), timed on this host's cores on a bounded sample
-    (a 2^log_c-constraint MiMC chain).  Its proof must equal the GPU's."""
+    (a 2^log_c-constraint MiMC chain, median of 3 after the port's own warm-up), plus a
+    1-thread figure on a smaller sample.  Its proofs must equal the GPU's."""
     from oracle import cpu_port
     rounds = (1 << (log_c - 1)) - 1
     params = bh.Parameters.chain(ctx, rounds)
@@ -60,11 +76,23 @@ def cpu_baseline(bh, ctx, log_c, gpu_params_cache):
     proof, ms, ms_syn = cpu_port.chain_prove(params.write(), rounds, threads=threads, reps=reps)
     wall = time.time() - t0
     n_c = 2 * rounds + 2
-    return {"value": round(n_c / (ms / 1e3), 1), "unit": "constraints/s", "cores": threads, "kind": "port",
-            "sample": f"median of {reps} prover-core runs (assignment -> proof) of a 2^{log_c}-constraint "
-                      f"MiMC chain; bellman's multicore algorithm restated in C++ (oracle/cpu); "
-                      f"{wall:.1f} s CPU wall incl. synthesis",
-            "ms_per_proof": round(ms, 1), "proof_matches_gpu": proof == gpu_proof}
+    out = {"value": round(n_c / (ms / 1e3), 1), "unit": "constraints/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
+           "sample": f"median of {reps} prover-core runs (assignment -> proof) of a 2^{log_c}-constraint "
+                     f"MiMC chain; bellman's multicore algorithm restated in C++ (oracle/cpu); "
+                     f"{wall:.1f} s CPU wall incl. synthesis",
+           "ms_per_proof": round(ms, 1), "synthesis_ms": round(ms_syn, 1),
+           "end_to_end_value": round(n_c / ((ms + ms_syn) / 1e3), 1),
+           "proof_matches_gpu": proof == gpu_proof}
+    if log_c_1t:
+        r1 = (1 << (log_c_1t - 1)) - 1
+        p1 = bh.Parameters.chain(ctx, r1)
+        g1 = bh.prove_witness(ctx, p1, bh.Witness.chain(ctx, r1), 27134, 17146)
+        proof1, ms1, _ = cpu_port.chain_prove(p1.write(), r1, threads=1, reps=3)
+        out["one_thread"] = {"value": round((2 * r1 + 2) / (ms1 / 1e3), 1), "unit": "constraints/s",
+                             "sample": f"median of 3, 2^{log_c_1t}-constraint chain, 1 thread",
+                             "proof_matches_gpu": proof1 == g1}
+    return out
 
 
 def main():
@@ -185,7 +213,19 @@ def main():
             "avg_launch_ms": round(acc_ms / launches, 4) if launches else None,
             "algorithmic_bytes_per_launch": round(pairs * G1_PAIR_BYTES / launches) if launches else None,
             "note": "VALU-bound (XYZZ mixed additions on 29-bit limbs): see DESIGN.md section 4"}
-    base = cpu_baseline(bh, ctx, args.cpu_log_constraints, None) if args.cpu_baseline else None
+    # integer-ALU roofline: G1 mixed additions/s against the microbenchmarked peak, and the
+    # v_mad_u64_u32 issue rate they imply (8 Fp-mul x 391 + 2 Fp-sqr x 300 per addition)
+    g1_adds = sum(t[8] for t in timings)
+    madd_rate = g1_adds / (acc_ms / 1e3) / 1e9 if acc_ms > 0 else None
+    valu = {"kernel": "k_accumulate_pf<G1>", "unit": "G mixed-add/s",
+            "achieved": round(madd_rate, 3) if madd_rate else None, "peak": G1_MADD_PEAK,
+            "frac": round(madd_rate / G1_MADD_PEAK, 4) if madd_rate else None,
+            "peak_source": "tools/microbench/curvebench.hip (L2-resident bases, 2 waves/SIMD)",
+            "mad_u64_tps": round(madd_rate * MADS_PER_G1_MADD / 1e3, 2) if madd_rate else None,
+            "mad_u64_frac": round(madd_rate * MADS_PER_G1_MADD / 1e3 / MAD_U64_PEAK_TPS, 4) if madd_rate else None,
+            "mad_u64_peak_tps": MAD_U64_PEAK_TPS, "mad_u64_peak_source": "tools/microbench/madbench.hip"}
+    base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints)
+            if args.cpu_baseline else None)
     out = {
         "metric": "Groth16 constraints/sec, BLS12-381, 2^22-constraint R1CS",
         "value": round(value, 1),
@@ -203,6 +243,9 @@ def main():
                    "constraints": n_constraints, "log_domain": k, "parallelism": f"msm-shard{world}",
                    "exchange": exchange if world > 1 else None},
         "roofline": roof,
+        "valu_roofline": valu,
+        "end_to_end": {"value": round(n_constraints / (t_wit + ms / 1e3), 1), "unit": "constraints/s",
+                       "note": "host witness synthesis (single thread, native) + upload + prover core"},
         "cpu_baseline": base,
         "breakdown_ms": {"h_pipeline": round(sum(t[1] for t in timings) / len(timings), 3),
                          "g1_accumulate": round(acc_ms / len(timings), 3),

@@ -50,7 +50,8 @@ typedef int bh_status;
 #define BH_ERR_UNCONSTRAINED_VARIABLE 5  /* generator.rs:582-586 */
 #define BH_ERR_INVALID_ARGUMENT 10
 #define BH_ERR_INVALID_ENCODING 11       /* IoError(InvalidData) of Parameters::read */
-#define BH_ERR_NOT_ON_CURVE 12
+#define BH_ERR_NOT_ON_CURVE 12          /* the checked decoders' InvalidData (mod.rs:292-400) */
+#define BH_ERR_NOT_IN_SUBGROUP 14       /* same reference error: not torsion-free */
 #define BH_ERR_OUT_OF_MEMORY 13
 #define BH_ERR_HIP 100                   /* HIP runtime / device failure */
 
@@ -172,8 +173,11 @@ bh_status bh_chain_params(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t al
 /* Parameters::write of device-resident params (for parity tests; host copy). */
 bh_status bh_params_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written);
 
-/* ---- timing of the last bh_prove_witness (device events on the prover stream), ms */
-bh_status bh_last_timings(const bh_ctx* ctx, double out[8]);
+/* ---- profile of the last bh_prove_witness[_partial] (device events):
+ * [0] host wall ms, [1] H pipeline ms, [2] G1 accumulation ms (sum over launches),
+ * [3] G1 accumulation launches, [4] G1 (base, scalar) pairs, [5] G2 accumulation ms,
+ * [6] G2 launches, [7] G2 pairs, [8] G1 mixed additions, [9] G2 mixed additions */
+bh_status bh_last_timings(const bh_ctx* ctx, double out[10]);
 
 #ifdef __cplusplus
 }

@@ -273,3 +273,28 @@ def test_window_tables_match_plain_windows(ctx, logc):
     assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
     if logc == 22:
         assert plain.hex().startswith("b320c6a265000d01babba804dc37ae10")
+
+
+def test_checked_load_rejects_points_outside_subgroup(ctx):
+    """Parameters::read(checked) / from_uncompressed reject on-curve points that are not
+    torsion-free (groth16/mod.rs:292-400); the unchecked read accepts them.  Fixture:
+    tests/golden/make_subgroup.py."""
+    import json
+    import os
+    bh = _bh()
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "subgroup.json")))
+    for group, key in ((bh.BH_G1, "g1_off_subgroup"), (bh.BH_G2, "g2_off_subgroup")):
+        raw = bytes.fromhex(fx[key])
+        with pytest.raises(bh.SynthesisError) as e:
+            bh.Bases(ctx, group, raw, checked=True)
+        assert e.value.code == 14
+        bh.Bases(ctx, group, raw, checked=False)
+    # a valid subgroup point passes the checked path
+    g = bytes.fromhex(_golden_first_g1())
+    bh.Bases(ctx, bh.BH_G1, g, checked=True)
+
+
+def _golden_first_g1():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["msm_g1"]["bases"][0]

@@ -221,3 +221,17 @@ def test_chain_circuit_shape():
         assert pr.b_input_density.get_total_density() == 1
         for x, y, z in zip(pr.a, pr.b, pr.c):
             assert x * y % q == z
+
+
+def test_subgroup_fixture_is_on_curve_but_not_torsion_free():
+    """tests/golden/subgroup.json: the oracle's checked decoders reject it, unchecked accept."""
+    import json
+    import os
+    from oracle import bls12_381 as bls
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "subgroup.json")))
+    for key, dec, C in (("g1_off_subgroup", bls.g1_from_uncompressed, bls.G1),
+                        ("g2_off_subgroup", bls.g2_from_uncompressed, bls.G2)):
+        raw = bytes.fromhex(fx[key])
+        ok, pt = dec(raw, checked=False)
+        assert ok and C.on_curve_affine(pt)
+        assert not dec(raw, checked=True)[0]
