@@ -614,4 +614,39 @@ int bp_chain_prove(const uint8_t* params, size_t len, size_t rounds, uint64_t se
 
 int bp_hardware_threads(void) { return (int)std::thread::hardware_concurrency(); }
 
+// multiexp::multiexp over G1 with FullDensity (multiexp.rs:252-281), bellman's schedule:
+// one task per window on a pool of `threads`.  bases: n_bases uncompressed encodings;
+// exps: n canonical scalars (4 LE u64).  out: uncompressed result (0x40 flag = identity).
+// Returns 0, 1 (identity base), 2 (EOF) or 11 (bad encoding).
+int bp_multiexp_g1(const uint8_t* bases, size_t n_bases, const uint64_t* exps, size_t n, int threads,
+                   uint8_t out[96], double* ms) {
+  std::vector<Aff<Fp>> b(n_bases);
+  for (size_t i = 0; i < n_bases; i++)
+    if (!read_g1(bases + 96 * i, &b[i])) return 11;
+  std::vector<Fb> e(n);
+  for (size_t i = 0; i < n; i++) memcpy(e[i].w, exps + 4 * i, 32);
+  Pool pool(threads > 0 ? threads : (int)std::thread::hardware_concurrency());
+  auto t0 = std::chrono::steady_clock::now();
+  MultiexpJob<Fp> job;
+  job.bases = &b;
+  job.offset = 0;
+  job.density = nullptr;
+  job.exps = &e;
+  multiexp_spawn<Fp>(pool, &job);
+  pool.wait_all();
+  if (job.err) return job.err;
+  multiexp_finish<Fp>(&job);
+  auto t1 = std::chrono::steady_clock::now();
+  if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  const Aff<Fp> a = to_affine(job.result);
+  memset(out, 0, 96);
+  if (a.inf) {
+    out[0] = 0x40;
+  } else {
+    to_be(a.x, out);
+    to_be(a.y, out + 48);
+  }
+  return 0;
+}
+
 }  // extern "C"

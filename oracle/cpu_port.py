@@ -25,6 +25,8 @@ def _lib():
     lib.bp_chain_prove.restype = I
     lib.bp_chain_prove.argtypes = [P, S, S, U64, I, I, P, P, P, P, P]
     lib.bp_hardware_threads.restype = I
+    lib.bp_multiexp_g1.restype = I
+    lib.bp_multiexp_g1.argtypes = [P, S, P, S, I, P, P]
     return lib
 
 
@@ -48,3 +50,19 @@ def chain_prove(params_bytes, rounds, seed=7, threads=0, reps=1, r=27134, s=1714
     if st != 0:
         raise RuntimeError(f"bellman port failed with status {st}")
     return out.tobytes(), ms.value, ms_syn.value
+
+
+def multiexp_g1(bases_uncompressed, exps_limbs, threads=0):
+    """bellman's multiexp (FullDensity) on the host cores: bases = concatenated 96-byte
+    uncompressed encodings, exps = (n,4) uint64 canonical limbs.  Returns (bytes, ms)."""
+    lib = _lib()
+    b = np.frombuffer(bases_uncompressed, dtype=np.uint8)
+    e = np.ascontiguousarray(exps_limbs, dtype=np.uint64).reshape(-1, 4)
+    out = np.zeros(96, dtype=np.uint8)
+    ms = ctypes.c_double()
+    st = lib.bp_multiexp_g1(b.ctypes.data_as(ctypes.c_void_p), len(bases_uncompressed) // 96,
+                            e.ctypes.data_as(ctypes.c_void_p), e.shape[0], threads,
+                            out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ms))
+    if st:
+        raise RuntimeError(f"bp_multiexp_g1 failed: {st}")
+    return out.tobytes(), ms.value

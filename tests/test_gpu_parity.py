@@ -298,3 +298,38 @@ def _golden_first_g1():
     import json
     import os
     return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["msm_g1"]["bases"][0]
+
+
+def _params_vectors(raw):
+    """Split Parameters::write bytes (groth16/mod.rs:260-290) -> dict of raw vectors."""
+    import struct
+    off = 96 + 96 + 192 + 192 + 96 + 192
+    (n_ic,) = struct.unpack(">I", raw[off:off + 4])
+    off += 4 + 96 * n_ic
+    out = {}
+    for name, size in (("h", 96), ("l", 96), ("a", 96), ("b_g1", 96), ("b_g2", 192)):
+        (n,) = struct.unpack(">I", raw[off:off + 4])
+        out[name] = raw[off + 4:off + 4 + n * size]
+        off += 4 + n * size
+    return out
+
+
+def test_c2_msm_2p20_matches_bellman_port(ctx):
+    """BASELINE.json configs[1] (C2): a 2^20-point G1 multiexp with dense uniform scalars,
+    bit-exact against bellman's multiexp algorithm (the C++ port, oracle/cpu) at full size.
+    Bases: the h query of a device-generated 2^21-constraint CRS ([tau^i Z(tau)/delta] G1)."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import cpu_port
+    bh = _bh()
+    n = 1 << 20
+    params = bh.Parameters.chain(ctx, (1 << 20) - 1)
+    h = _params_vectors(params.write())["h"][:96 * n]
+    rng = np.random.default_rng(20)
+    ex = rng.integers(0, 1 << 63, size=(n, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+    ex[:, 3] %= np.uint64(0x73EDA753299D7D48)  # below r
+    bases = bh.Bases(ctx, bh.BH_G1, h, checked=False)
+    got = bh.multiexp(ctx, bases, 0, None, ex)
+    want, _ = cpu_port.multiexp_g1(h, ex)
+    assert got == want
