@@ -114,6 +114,7 @@ def _load():
         "bh_device_count": (I, []),
         "bh_ctx_set_tables": (I, [P, I]),
         "bh_params_prepare": (I, [P, P, P, S]),
+        "bh_chain_witness_preimage": (I, [P, S, U64, U64, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -134,6 +135,7 @@ EXPORTED_SYMBOLS = [
     "bh_chain_params", "bh_params_write", "bh_last_timings", "bh_shard_range", "bh_prove_witness_partial",
     "bh_vk_write", "bh_proof_from_partials", "bh_comm_unique_id", "bh_comm_init", "bh_comm_allgather_partials",
     "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count", "bh_ctx_set_tables", "bh_params_prepare",
+    "bh_chain_witness_preimage",
 ]
 PARTIAL_BYTES = 960
 
@@ -541,9 +543,12 @@ class Witness:
         return cls(ctx, h, len(p.a))
 
     @classmethod
-    def chain(cls, ctx, rounds, seed=7):
+    def chain(cls, ctx, rounds, seed=7, preimage_seed=None):
+        """Native MiMC-chain synthesis: constants from seed, preimage from preimage_seed
+        (default seed + 1)."""
         h = ctypes.c_void_p()
-        _check(_lib.bh_chain_witness(ctx.h, rounds, seed, ctypes.byref(h)), "bh_chain_witness")
+        ps = seed + 1 if preimage_seed is None else preimage_seed
+        _check(_lib.bh_chain_witness_preimage(ctx.h, rounds, seed, ps, ctypes.byref(h)), "bh_chain_witness")
         return cls(ctx, h, 2 * rounds + 2)
 
     def __del__(self):

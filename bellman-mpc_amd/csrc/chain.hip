@@ -252,9 +252,14 @@ bh_status fixed_base_to_srs(bh_ctx* ctx, const std::vector<AffinePt<T>>& table, 
 extern "C" {
 
 bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness** out) {
+  return bh_chain_witness_preimage(ctx, rounds, seed, seed + 1, out);
+}
+
+bh_status bh_chain_witness_preimage(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t preimage_seed,
+                                    bh_witness** out) {
   if (!ctx || !out || rounds == 0) return BH_ERR_INVALID_ARGUMENT;
   const std::vector<Fr> consts = fr_stream(seed, rounds);
-  const std::vector<Fr> pre = fr_stream(seed + 1, 2);
+  const std::vector<Fr> pre = fr_stream(preimage_seed, 2);
   ProvingAssignmentN cs;
   const size_t nc = 2 * rounds + 2;
   cs.a.reserve(nc); cs.b.reserve(nc); cs.c.reserve(nc);

@@ -168,6 +168,11 @@ int bh_device_count(void);
  * synthesized natively (witness) and its CRS generated on the device with the classic
  * algorithm (generator.rs:310-572) from the given toxic waste (canonical u64 each). */
 bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness** out);
+/* Same circuit (constants from seed), preimage (xl, xr) from preimage_seed: distinct
+ * witnesses for one set of Parameters (BASELINE.json configs[4], "C5").
+ * bh_chain_witness(seed) == bh_chain_witness_preimage(seed, seed + 1). */
+bh_status bh_chain_witness_preimage(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t preimage_seed,
+                                    bh_witness** out);
 bh_status bh_chain_params(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t alpha, uint64_t beta, uint64_t gamma,
                           uint64_t delta, uint64_t tau, bh_params** out);
 /* Parameters::write of device-resident params (for parity tests; host copy). */

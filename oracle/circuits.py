@@ -78,12 +78,13 @@ class MiMCDemo:
             xl, xl_value = new_xl, new_xl_value
 
 
-def chain_circuit(q, rounds, seed=7, witness=True):
+def chain_circuit(q, rounds, seed=7, witness=True, preimage_seed=None):
     """Synthetic MiMC chain: constants = fr_stream(seed, R); (xl, xr) =
-    fr_stream(seed + 1, 2).  Mirrors bh_chain_* in the native synthesizer."""
+    fr_stream(preimage_seed, 2), preimage_seed defaulting to seed + 1.  Mirrors
+    bh_chain_* in the native synthesizer."""
     consts = fr_stream(seed, rounds, q)
     if witness:
-        xl, xr = fr_stream(seed + 1, 2, q)
+        xl, xr = fr_stream(seed + 1 if preimage_seed is None else preimage_seed, 2, q)
     else:
         xl = xr = None
     return MiMCDemo(xl, xr, consts, q)

@@ -333,3 +333,52 @@ def test_c2_msm_2p20_matches_bellman_port(ctx):
     got = bh.multiexp(ctx, bases, 0, None, ex)
     want, _ = cpu_port.multiexp_g1(h, ex)
     assert got == want
+
+
+def test_c5_distinct_witnesses_shared_params(ctx):
+    """BASELINE.json configs[4] (C5) semantics: independent proofs of one circuit (shared
+    Parameters) with distinct witnesses, each bit-exact with the oracle."""
+    from oracle import bellman as bm
+    from oracle import bls12_381 as bls
+    from oracle import circuits as cc
+    bh = _bh()
+    E = bm.BLS12_381
+    for rounds in (3, 15):
+        oparams = bm.generate_random_parameters(E, cc.chain_circuit(bls.R, rounds, witness=False))
+        params = bh.Parameters.chain(ctx, rounds)
+        assert params.write() == bm.params_to_bytes(oparams)
+        for ps in (100, 101, 102, 103):
+            prover = bm.synthesize_for_proving(E, cc.chain_circuit(bls.R, rounds, preimage_seed=ps))
+            want = bm.proof_to_bytes(bm.prove_from_assignment(E, prover, oparams, 27134, 17146))
+            w = bh.Witness.chain(ctx, rounds, preimage_seed=ps)
+            assert bh.prove_witness(ctx, params, w, 27134, 17146) == want, (rounds, ps)
+
+
+def test_concurrent_contexts_in_threads(golden):
+    """Throughput mode (C5): several contexts on one device proving at once from host
+    threads (the ABI is thread-safe per context; ctypes releases the GIL) give the same
+    bytes as the committed proof."""
+    import threading
+    bh = _bh()
+    fx = [f for f in golden["proofs"] if f["name"] == "mimc_chain_r15"][0]
+    results, errors = [], []
+
+    def worker():
+        try:
+            c = bh.Context(0)
+            p = bh.Parameters.chain(c, 15)
+            w = bh.Witness.chain(c, 15)
+            for _ in range(3):
+                results.append(bh.prove_witness(c, p, w, 27134, 17146).hex())
+            del p, w
+            c.close()
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=worker) for _ in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    assert len(results) == 12 and set(results) == {fx["proof"]}
