@@ -382,3 +382,24 @@ def test_concurrent_contexts_in_threads(golden):
         t.join()
     assert not errors, errors
     assert len(results) == 12 and set(results) == {fx["proof"]}
+
+
+@pytest.mark.slow
+def test_c4_2p24_sharded_8_ways_equals_single_device_proof():
+    """BASELINE.json configs[3] (C4): a 2^24-constraint proof whose multiexps are split 8 ways
+    by scalar range (bh_prove_witness_partial, the per-rank work of the multi-GPU path, run
+    here shard after shard on one device) and recombined by bh_proof_from_partials equals
+    the unsharded proof.  Both use SRS window tables sized for their shard (c differs)."""
+    bh = _bh()
+    c = bh.Context(0)
+    try:
+        rounds = (1 << 23) - 1
+        params = bh.Parameters.chain(c, rounds)
+        w = bh.Witness.chain(c, rounds)
+        single = bh.prove_witness(c, params, w, 27134, 17146)
+        params.prepare(w, 8)
+        parts = b"".join(bh.prove_witness_partial(c, params, w, k, 8) for k in range(8))
+        assert bh.proof_from_partials(params.vk_bytes(), parts, 8, 27134, 17146) == single
+        del params, w
+    finally:
+        c.close()
