@@ -550,6 +550,13 @@ const char* bh_status_string(bh_status s) {
 
 int bh_version(void) { return 1; }
 
+// The prover keeps 12 streams in flight (accumulations, sorts, H, small multiexps and one
+// reduction tail per large multiexp).  HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+// queues (default 4); streams sharing a queue serialise behind each other's event waits,
+// which would queue every tail behind the next accumulation.  Ask for 16 queues unless the
+// host already chose a value; this runs when the library is loaded, before any HIP call.
+__attribute__((constructor)) static void bh_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "16", 0); }
+
 bh_status bh_ctx_create(int device, bh_ctx** out) {
   if (!out) return BH_ERR_INVALID_ARGUMENT;
   int count = 0;
@@ -560,14 +567,21 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { delete c; return BH_ERR_HIP; }
-  const char* pe = getenv("BH_SIDE_PRIORITY");  // experiment knob: 1 = side streams at high priority
-  const int side = (pe && pe[0] == '1') ? prio_hi : prio_lo;
+  // side streams (sorts, H pipeline, reduction tails) at high priority; BH_SIDE_PRIORITY=0
+  // puts them at the default priority (A/B experiments)
+  const char* pe = getenv("BH_SIDE_PRIORITY");
+  const int side = (pe && pe[0] == '0') ? prio_lo : prio_hi;
   if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess) {
     delete c;
     return BH_ERR_HIP;
   }
+  for (auto& t : c->tstream)
+    if (hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess) {
+      delete c;
+      return BH_ERR_HIP;
+    }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
@@ -603,6 +617,10 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream4);
+  for (auto& t : ctx->tstream) {
+    (void)hipStreamSynchronize(t);
+    (void)hipStreamDestroy(t);
+  }
   delete ctx;
   return BH_OK;
 }

@@ -102,6 +102,7 @@ struct bh_ctx {
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
+  hipStream_t tstream[8] = {};     // prover: one reduction-tail stream per large multiexp (high priority)
   int window_override = 0;
   int tables = 1;  // 1: the prover builds and uses SRS window tables (bh_ctx_set_tables)
   bh::MsmWorkspace<G1Ops> g1ws;

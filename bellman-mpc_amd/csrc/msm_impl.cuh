@@ -279,8 +279,16 @@ void fit_segments(MsmShape& sh, size_t n) {
     const int r = e ? atoi(e) : 4;
     return (size_t)(r > 0 ? r : 4);
   }();
+  // BH_ACC_FILL: fraction of the resident capacity the accumulation occupies per round
+  // (the rest stays free for the side streams' short kernels)
+  static const double fill = [] {
+    const char* e = getenv("BH_ACC_FILL");
+    const double f = e ? atof(e) : 1.0;
+    return (f > 0.0 && f <= 1.0) ? f : 1.0;
+  }();
   const size_t E = n * (size_t)sh.W;
-  size_t S = (E + rounds * conc - 1) / (rounds * conc);
+  const size_t slots = std::max<size_t>((size_t)(rounds * conc * fill) / 256 * 256, 256);
+  size_t S = (E + slots - 1) / slots;
   sh.S = (int)std::min<size_t>(std::max<size_t>(S, 8), (size_t)1 << 16);
 }
 

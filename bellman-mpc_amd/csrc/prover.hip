@@ -334,19 +334,24 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (s) return s;
     }
   }
-  // Four streams, all ordered after whatever ran before on ctx->stream:
-  //   stream : the bucket accumulations back to back (VALU-bound critical path);
-  //   stream4: the small (public-input) multiexps, the H pipeline (after the first
-  //            accumulation), then the G2 reduction tails;
-  //   stream3: density maps, then every multiexp's sort (memory-bound, runs ahead);
-  //   stream2: the G1 reduction tails, each as soon as its multiexp is accumulated.
+  // Streams, all ordered after whatever ran before on ctx->stream:
+  //   stream    : the bucket accumulations back to back (VALU-bound critical path);
+  //   stream4   : the H pipeline (by default alone at the start, see h_first below);
+  //   stream3   : density maps, then every multiexp's sort (memory-bound, runs ahead);
+  //   stream2   : the small (public-input) multiexps, whole;
+  //   tstream[q]: the reduction tail of the q-th large multiexp.
   // Each multiexp has its own workspace, so the only dependencies are the events below.
   hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
+  hipStream_t tails[8];
+  for (int q = 0; q < 8; q++) tails[q] = ctx->tstream[q];
   static const bool serial = [] {  // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
     const char* e = getenv("BH_PROVER_SERIAL");
     return e && e[0] == '1';
   }();
-  if (serial) sT = sS = sH = sA;
+  if (serial) {
+    sT = sS = sH = sA;
+    for (auto& t : tails) t = sA;
+  }
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated,
                                // [32] start, [33] density maps ready
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
@@ -374,14 +379,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     size_t used;           // density-set scalars (roofline accounting)
     int out;               // result slot: G1 0..5 / G2 0..1
   };
-  // G2 first (the longest tail gets the most overlap), h fourth so H has two
+  // G2 first (the longest tail gets the most overlap), h last so the H pipeline has three
   // accumulations of slack
   const Job jobs[8] = {
       {true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1},              // b_g2_aux
       {false, &params->l, aux, na, nullptr, na, 1},                             // l
       {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
-      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
       {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
+      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
       {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
       {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
       {true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0},             // b_g2_inputs
@@ -450,50 +455,79 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out));
     return BH_OK;
   };
-  // Small multiexps (the public-input queries) are latency-bound: run them whole on the
-  // H stream first, inside the start-up gap, after the density maps.
   BH_TRY_HIP(hipEventRecord(jev[33], sS));
   BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
-  int big[8], nbig = 0;
+  int big[8], nbig = 0, small[8], nsmall = 0;
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];
     if (!n) continue;
-    if (n < SMALL_JOB && jobs[j].sc != ctx->hbuf.as<uint32_t>()) {
-      if ((s = sort_job(j, sH)) || (s = acc_job(j, sH)) || (s = tail_job(j, sH))) return s;
-    } else {
-      big[nbig++] = j;
-    }
+    if (n < SMALL_JOB && jobs[j].sc != ctx->hbuf.as<uint32_t>()) small[nsmall++] = j;
+    else big[nbig++] = j;
   }
   // Large ones: sorts run ahead on stream3, accumulations back to back on the main stream,
-  // each tail on a side stream (G2 tails on the H stream, so they never hold up G1 tails).
-  // H starts once the first accumulation is done -- earlier it keeps CUs from the first,
-  // whole-CU G2 accumulation -- and is needed only by h's sort, two accumulations later.
+  // each reduction tail on a stream of its own (the tails are latency-bound chains of point
+  // additions: several run side by side at little cost, and none waits behind another).
   int h_pos = nbig;
   for (int q = 0; q < nbig; q++)
     if (jobs[big[q]].sc == ctx->hbuf.as<uint32_t>()) h_pos = q;
-  for (int q = 0; q < h_pos; q++)
-    if ((s = sort_job(big[q], sS))) return s;
+  // H first (default): the pipeline runs alone at the start, next to the memory-bound sorts,
+  // and the first accumulation waits for it.  Run concurrently with an accumulation, its
+  // short NTT passes only get CUs as accumulation workgroups retire (stream priority does
+  // not change that) and it stretches from ~5 ms to ~30 ms, leaving h's accumulation waiting.
+  // BH_H_FIRST=0: H after the first accumulation, overlapped (A/B experiments).
+  static const bool h_first = [] {
+    const char* e = getenv("BH_H_FIRST");
+    return !(e && e[0] == '0');
+  }();
+  // the small multiexps run whole on their own stream, after the density maps
+  BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
+  auto run_small = [&]() -> bh_status {
+    for (int i = 0; i < nsmall; i++) {
+      bh_status e = sort_job(small[i], sT);
+      if (!e) e = acc_job(small[i], sT);
+      if (!e) e = tail_job(small[i], sT);
+      if (e) return e;
+    }
+    return BH_OK;
+  };
   int next_acc = 0;
-  if (h_pos > 0) {
-    if ((s = acc_job(big[0], sA))) return s;
-    if ((s = enqueue_h(jev[24 + big[0]]))) return s;  // ahead of the first tail on its stream
-    if ((s = tail_job(big[0], jobs[big[0]].g2 ? sH : sT))) return s;
-    next_acc = 1;
-  } else if ((s = enqueue_h(jev[33]))) {
-    return s;
-  }
-  for (int q = h_pos; q < nbig; q++) {
-    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    if ((s = sort_job(big[q], sS))) return s;
+  if (h_first) {
+    if ((s = enqueue_h(jev[33]))) return s;
+    for (int q = 0; q < nbig; q++) {
+      if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+      if ((s = sort_job(big[q], sS))) return s;
+    }
+    if ((s = run_small())) return s;
+    BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
+  } else {
+    // the first sort is enqueued before the small multiexps: it gates the first accumulation
+    for (int q = 0; q < h_pos; q++) {
+      if ((s = sort_job(big[q], sS))) return s;
+      if (q == 0 && (s = run_small())) return s;
+    }
+    if (h_pos == 0 && (s = run_small())) return s;
+    if (h_pos > 0) {
+      if ((s = acc_job(big[0], sA))) return s;
+      if ((s = enqueue_h(jev[24 + big[0]]))) return s;  // ahead of the first tail on its stream
+      if ((s = tail_job(big[0], tails[0]))) return s;
+      next_acc = 1;
+    } else if ((s = enqueue_h(jev[33]))) {
+      return s;
+    }
+    for (int q = h_pos; q < nbig; q++) {
+      if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+      if ((s = sort_job(big[q], sS))) return s;
+    }
   }
   for (int q = next_acc; q < nbig; q++) {
     const int j = big[q];
-    if ((s = acc_job(j, sA)) || (s = tail_job(j, jobs[j].g2 ? sH : sT))) return s;
+    if ((s = acc_job(j, sA)) || (s = tail_job(j, tails[q]))) return s;
   }
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
   BH_TRY_HIP(hipStreamSynchronize(sH));
   BH_TRY_HIP(hipStreamSynchronize(sT));
+  for (int q = 0; q < nbig; q++) BH_TRY_HIP(hipStreamSynchronize(tails[q]));
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0, g1_adds = 0, g2_adds = 0;
   int g1_launches = 0, g2_launches = 0;
