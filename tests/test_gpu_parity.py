@@ -403,3 +403,26 @@ def test_c4_2p24_sharded_8_ways_equals_single_device_proof():
         del params, w
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("logc", [10, 22])
+def test_device_proof_verifies_with_pairing(ctx, logc):
+    """The device proof of a MiMC chain -- at 2^22 constraints the benchmark's own proof
+    (BASELINE.json configs[2]) -- is accepted by the oracle's restatement of verify_proof
+    (verifier.rs:23-62, oracle/pairing.py) for the device-generated verifying key and the
+    chain's public image, and rejected for a wrong image."""
+    from oracle import bls12_381 as bls
+    from oracle import circuits as cc
+    from oracle import pairing as pr
+    bh = _bh()
+    rounds = (1 << (logc - 1)) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    params.prepare(w)
+    proof = pr.proof_from_bytes(bh.prove_witness(ctx, params, w, 27134, 17146))
+    vk_bytes = params.vk_bytes()
+    vk = pr.vk_from_params_bytes(vk_bytes)
+    xl, xr = cc.fr_stream(8, 2, bls.R)
+    image = cc.mimc(xl, xr, cc.fr_stream(7, rounds, bls.R), bls.R)
+    assert pr.verify_proof(vk, proof, [image])
+    assert not pr.verify_proof(vk, proof, [(image + 1) % bls.R])
