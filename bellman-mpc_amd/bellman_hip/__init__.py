@@ -115,6 +115,8 @@ def _load():
         "bh_ctx_set_tables": (I, [P, I]),
         "bh_params_prepare": (I, [P, P, P, S]),
         "bh_chain_witness_preimage": (I, [P, S, U64, U64, P]),
+        "bh_prove_witness_partial_comm": (I, [P, P, P, P, P]),
+        "bh_prove_witness_partials_local": (I, [P, P, P, S, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -135,7 +137,7 @@ EXPORTED_SYMBOLS = [
     "bh_chain_params", "bh_params_write", "bh_last_timings", "bh_shard_range", "bh_prove_witness_partial",
     "bh_vk_write", "bh_proof_from_partials", "bh_comm_unique_id", "bh_comm_init", "bh_comm_allgather_partials",
     "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count", "bh_ctx_set_tables", "bh_params_prepare",
-    "bh_chain_witness_preimage",
+    "bh_chain_witness_preimage", "bh_prove_witness_partial_comm", "bh_prove_witness_partials_local",
 ]
 PARTIAL_BYTES = 960
 
@@ -592,6 +594,14 @@ def prove_witness_partial(ctx, params, witness, shard, nshards):
     return out.tobytes()
 
 
+def prove_witness_partials_local(ctx, params, witness, nshards):
+    """All nshards partial records on this one device (distributed H emulated with device
+    copies): the multi-GPU algorithm end to end without a second GPU."""
+    out = np.zeros(nshards * PARTIAL_BYTES, dtype=np.uint8)
+    _check(_lib.bh_prove_witness_partials_local(ctx.h, params.h, witness.h, nshards, _ptr(out)), "partials_local")
+    return out.tobytes()
+
+
 def proof_from_partials(vk_bytes, partials, nshards, r, s):
     """Host-only: sum the gathered partials (shard order) and assemble the proof."""
     vk = np.frombuffer(vk_bytes, dtype=np.uint8)
@@ -622,6 +632,13 @@ class Comm:
         h = ctypes.c_void_p()
         _check(_lib.bh_comm_init(ctx.h, _ptr(b), nranks, rank, ctypes.byref(h)), "ncclCommInitRank")
         self.h, self.nranks = h, nranks
+
+    def prove_partial(self, ctx, params, witness):
+        """This rank's partial record with the H block distributed over the communicator
+        (bh_prove_witness_partial_comm)."""
+        out = np.zeros(PARTIAL_BYTES, dtype=np.uint8)
+        _check(_lib.bh_prove_witness_partial_comm(ctx.h, params.h, witness.h, self.h, _ptr(out)), "partial_comm")
+        return out.tobytes()
 
     def allgather(self, partial):
         src = np.frombuffer(partial, dtype=np.uint8)

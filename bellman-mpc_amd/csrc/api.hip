@@ -8,6 +8,7 @@
 #include <chrono>
 
 #include "api_internal.h"
+#include "dist_h.h"
 
 using namespace bh;
 
@@ -621,6 +622,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
     (void)hipStreamSynchronize(t);
     (void)hipStreamDestroy(t);
   }
+  delete ctx->dist;
   delete ctx;
   return BH_OK;
 }

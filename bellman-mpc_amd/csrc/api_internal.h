@@ -61,6 +61,7 @@ struct Domain {
 };
 
 struct bh_ctx_impl;
+struct DistH;
 }  // namespace bh
 
 struct bh_srs {
@@ -103,6 +104,7 @@ struct bh_ctx {
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
   hipStream_t tstream[8] = {};     // prover: one reduction-tail stream per large multiexp (high priority)
+  bh::DistH* dist = nullptr;       // prover: this rank's distributed-H state (bh_prove_witness_partial_comm)
   int window_override = 0;
   int tables = 1;  // 1: the prover builds and uses SRS window tables (bh_ctx_set_tables)
   bh::MsmWorkspace<G1Ops> g1ws;
@@ -151,4 +153,13 @@ bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n,
 bh_status multiexp_check(const bh_srs* bases, size_t base_offset, const uint64_t* density_words, size_t n,
                          const uint64_t* exps_canonical, bool need_exps);
 bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_affine_g1_or_g2, size_t n, bh_srs* out);
+// RCCL all-to-all of C-element packed-Fr chunks for the distributed H pipeline: for each of
+// nvec vectors of M = N*C elements, chunk p of send goes to rank p, which stores it as chunk
+// `this rank` of recv (comm.cpp)
+bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
+                        hipStream_t st);
+// smallest rank count that uses the distributed H pipeline (BH_DIST_H_MIN, default 4)
+size_t dist_h_min_ranks();
+int comm_rank(const bh_comm* c);
+int comm_size(const bh_comm* c);
 }  // namespace bh

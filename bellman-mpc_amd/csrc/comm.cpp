@@ -6,6 +6,7 @@
 // replacement for its single-process rayon fan-out (prover.rs:233-307).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "api_internal.h"
@@ -60,6 +61,49 @@ bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t
   BH_TRY_HIP(hipStreamSynchronize(st));
   return BH_OK;
 }
+
+}  // extern "C"
+
+namespace bh {
+
+size_t dist_h_min_ranks() {
+  static const size_t v = [] {
+    const char* e = getenv("BH_DIST_H_MIN");
+    const long x = e ? atol(e) : 4;
+    return (size_t)(x > 1 ? x : 2);
+  }();
+  return v;
+}
+
+bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
+                        hipStream_t st) {
+  const size_t bytes = C * 32;
+  for (int v = 0; v < nvec; v++) {  // own chunk: a device copy
+    const size_t off = ((size_t)v * M + (size_t)c->rank * C) * 8;
+    BH_TRY_HIP(hipMemcpyAsync(recv + off, send + off, bytes, hipMemcpyDeviceToDevice, st));
+  }
+  if (ncclGroupStart() != ncclSuccess) return BH_ERR_HIP;
+  for (int v = 0; v < nvec; v++)
+    for (int p = 0; p < c->nranks; p++) {
+      if (p == c->rank) continue;
+      const uint32_t* s = send + ((size_t)v * M + (size_t)p * C) * 8;
+      uint32_t* r = recv + ((size_t)v * M + (size_t)p * C) * 8;
+      if (ncclSend(s, bytes, ncclUint8, p, c->comm, st) != ncclSuccess ||
+          ncclRecv(r, bytes, ncclUint8, p, c->comm, st) != ncclSuccess) {
+        ncclGroupEnd();
+        return BH_ERR_HIP;
+      }
+    }
+  if (ncclGroupEnd() != ncclSuccess) return BH_ERR_HIP;
+  return BH_OK;
+}
+
+int comm_rank(const bh_comm* c) { return c->rank; }
+int comm_size(const bh_comm* c) { return c->nranks; }
+
+}  // namespace bh
+
+extern "C" {
 
 bh_status bh_comm_destroy(bh_comm* c) {
   if (!c) return BH_OK;

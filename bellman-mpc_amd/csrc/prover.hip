@@ -7,6 +7,7 @@
 
 #include "api_internal.h"
 #include "crs.h"
+#include "dist_h.h"
 
 using namespace bh;
 
@@ -290,10 +291,18 @@ bh_status prepare_tables(bh_ctx* ctx, bh_params* params, size_t m, size_t na, si
   return ensure_table(ctx, &params->b_g2, table_c_for(b_aux_used / N));
 }
 
+// Where this shard's h scalars come from when they are not the replicated H pipeline's
+// range [shard*(m-1)/N, ...): a precomputed share (hbuf/hidx of a finished DistH, used by
+// the one-device emulation), or the distributed pipeline run here over RCCL.
+struct HSource {
+  const DistH* pre = nullptr;  // finished share: hbuf (canonical) + hidx, M entries
+  bh_comm* comm = nullptr;     // run DistH over this communicator (rank/nranks = shard/nshards)
+};
+
 // `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
 // res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
 bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
-                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2]) {
+                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], const HSource& hsrc = HSource()) {
   const auto t0 = std::chrono::steady_clock::now();
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
   const int L = w->log_m;
@@ -378,7 +387,23 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const int32_t* idx;    // density map (already offset into the base vector) or null
     size_t used;           // density-set scalars (roofline accounting)
     int out;               // result slot: G1 0..5 / G2 0..1
+    bool is_h = false;     // h: needs the H pipeline
+    bool presharded = false;  // n/idx are this shard's already (distributed H)
   };
+  // distributed H: this rank ends with its own share of h (dist_h.h), no range split
+  DistH* dh = nullptr;
+  if (hsrc.comm && dist_h_eligible((int)nshards, L) && nshards >= dist_h_min_ranks()) {
+    if (!ctx->dist) ctx->dist = new DistH();
+    if ((s = dist_h_init(ctx, *ctx->dist, (int)nshards, (int)shard, L))) return s;
+    dh = ctx->dist;
+  }
+  const DistH* hshare = hsrc.pre ? hsrc.pre : dh;
+  Job hjob{false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0, true, false};
+  if (hshare) {
+    const size_t used = hshare->rank == hshare->N - 1 ? hshare->M - 1 : hshare->M;
+    hjob = Job{false, &params->h, hshare->hbuf.as<uint32_t>(), hshare->M, hshare->hidx.as<int32_t>(), used, 0, true,
+               true};
+  }
   // G2 first (the longest tail gets the most overlap), h last so the H pipeline has three
   // accumulations of slack
   const Job jobs[8] = {
@@ -386,7 +411,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       {false, &params->l, aux, na, nullptr, na, 1},                             // l
       {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
       {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
-      {false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0},  // h
+      hjob,                                                                     // h
       {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
       {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
       {true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0},             // b_g2_inputs
@@ -395,7 +420,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   bool use_table[8] = {false};
   size_t los[8], his[8];
   for (int j = 0; j < 8; j++) {
-    shard_range(jobs[j].n, shard, nshards, &los[j], &his[j]);
+    if (jobs[j].presharded) {
+      los[j] = 0;
+      his[j] = jobs[j].n;
+    } else {
+      shard_range(jobs[j].n, shard, nshards, &los[j], &his[j]);
+    }
     if (his[j] == los[j]) continue;
     const size_t used = (size_t)((unsigned __int128)jobs[j].used * (his[j] - los[j]) / std::max<size_t>(jobs[j].n, 1));
     const bh_srs* srs = jobs[j].srs;
@@ -411,6 +441,21 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   auto enqueue_h = [&](hipEvent_t after) -> bh_status {
     BH_TRY_HIP(hipStreamWaitEvent(sH, after, 0));
     hipEventRecord(ctx->ev[0], sH);
+    if (hsrc.pre) {  // share computed beforehand
+      hipEventRecord(ctx->ev[1], sH);
+      return BH_OK;
+    }
+    if (dh) {  // three all-to-alls over RCCL, stream-ordered on sH
+      bh_comm* cm = hsrc.comm;
+      const size_t chunk = dh->C, M = dh->M;
+      HExchange ex = [cm, chunk, M](const uint32_t* send, uint32_t* recv, int nvec, hipStream_t st) {
+        return comm_exchange(cm, send, recv, chunk, M, nvec, st);
+      };
+      bh_status hs = dist_h_run(ctx, *dh, w->abc.as<uint32_t>(), ex, sH);
+      if (hs) return hs;
+      hipEventRecord(ctx->ev[1], sH);
+      return BH_OK;
+    }
     uint32_t* abc = ctx->staging.as<uint32_t>();
     BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
     bh_status hs = run_h_pipeline(ctx, D, abc, sH);
@@ -461,7 +506,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];
     if (!n) continue;
-    if (n < SMALL_JOB && jobs[j].sc != ctx->hbuf.as<uint32_t>()) small[nsmall++] = j;
+    if (n < SMALL_JOB && !jobs[j].is_h) small[nsmall++] = j;
     else big[nbig++] = j;
   }
   // Large ones: sorts run ahead on stream3, accumulations back to back on the main stream,
@@ -469,7 +514,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // additions: several run side by side at little cost, and none waits behind another).
   int h_pos = nbig;
   for (int q = 0; q < nbig; q++)
-    if (jobs[big[q]].sc == ctx->hbuf.as<uint32_t>()) h_pos = q;
+    if (jobs[big[q]].is_h) h_pos = q;
   // H first (default): the pipeline runs alone at the start, next to the memory-bound sorts,
   // and the first accumulation waits for it.  Run concurrently with an accumulation, its
   // short NTT passes only get CUs as accumulation workgroups retire (stream priority does
@@ -601,6 +646,11 @@ VkHost vk_of(const bh_params* p) {
 
 constexpr size_t PARTIAL_BYTES = 6 * 96 + 2 * 192;
 
+void write_partial(const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], uint8_t* out) {
+  for (int i = 0; i < 6; i++) g1_to_uncompressed(jac_to_affine(r1[i]), out + 96 * i);
+  for (int i = 0; i < 2; i++) g2_to_uncompressed(jac_to_affine(r2[i]), out + 576 + 192 * i);
+}
+
 }  // namespace
 
 extern "C" {
@@ -642,8 +692,78 @@ bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const b
   Jac<bh::Fp2> r2[2];
   bh_status s = compute_msms(ctx, params, w, shard, nshards, r1, r2);
   if (s) return s;
-  for (int i = 0; i < 6; i++) g1_to_uncompressed(jac_to_affine(r1[i]), partial_out + 96 * i);
-  for (int i = 0; i < 2; i++) g2_to_uncompressed(jac_to_affine(r2[i]), partial_out + 576 + 192 * i);
+  write_partial(r1, r2, partial_out);
+  return BH_OK;
+}
+
+bh_status bh_prove_witness_partial_comm(bh_ctx* ctx, const bh_params* params, const bh_witness* w, bh_comm* comm,
+                                        uint8_t partial_out[960]) {
+  if (!ctx || !params || !w || !comm || !partial_out) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  HSource hs;
+  hs.comm = comm;
+  bh_status s = compute_msms(ctx, params, w, (size_t)comm_rank(comm), (size_t)comm_size(comm), r1, r2, hs);
+  if (s) return s;
+  write_partial(r1, r2, partial_out);
+  return BH_OK;
+}
+
+bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, const bh_witness* w,
+                                          size_t nshards, uint8_t* partials_out) {
+  if (!ctx || !params || !w || !partials_out || nshards == 0) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  const int N = (int)nshards;
+  std::vector<std::unique_ptr<DistH>> d;
+  if (dist_h_eligible(N, w->log_m)) {
+    // N virtual ranks on this device: the distributed H pipeline with device copies for the
+    // all-to-alls, each rank's share kept for its multiexps below
+    for (int k = 0; k < N; k++) {
+      d.emplace_back(new DistH());
+      bh_status s = dist_h_init(ctx, *d.back(), N, k, w->log_m);
+      if (s) return s;
+    }
+    hipStream_t st = ctx->stream;
+    const size_t C = d[0]->C, M = d[0]->M;
+    auto exchange = [&](bool from_work, int nvec) -> bh_status {
+      for (int dst = 0; dst < N; dst++)
+        for (int src = 0; src < N; src++)
+          for (int v = 0; v < nvec; v++) {
+            const uint32_t* sb = (from_work ? d[src]->work : d[src]->recv).as<uint32_t>();
+            uint32_t* rb = (from_work ? d[dst]->recv : d[dst]->work).as<uint32_t>();
+            BH_TRY_HIP(hipMemcpyAsync(rb + ((size_t)v * M + (size_t)src * C) * 8,
+                                      sb + ((size_t)v * M + (size_t)dst * C) * 8, C * 32, hipMemcpyDeviceToDevice,
+                                      st));
+          }
+      return BH_OK;
+    };
+    bh_status s;
+    const uint32_t* abc = w->abc.as<uint32_t>();
+    for (int k = 0; k < N; k++)
+      if ((s = dist_h_phase1(ctx, *d[k], abc, st))) return s;
+    if ((s = exchange(true, 3))) return s;
+    for (int k = 0; k < N; k++)
+      if ((s = dist_h_phase2(ctx, *d[k], st))) return s;
+    if ((s = exchange(true, 3))) return s;
+    for (int k = 0; k < N; k++)
+      if ((s = dist_h_phase3(ctx, *d[k], st))) return s;
+    if ((s = exchange(false, 1))) return s;
+    for (int k = 0; k < N; k++)
+      if ((s = dist_h_final(ctx, *d[k], st))) return s;
+    BH_TRY_HIP(hipStreamSynchronize(st));
+  }
+  for (int k = 0; k < N; k++) {
+    Jac<Fp> r1[6];
+    Jac<bh::Fp2> r2[2];
+    HSource hs;
+    hs.pre = d.empty() ? nullptr : d[k].get();
+    bh_status s = compute_msms(ctx, params, w, (size_t)k, nshards, r1, r2, hs);
+    if (s) return s;
+    write_partial(r1, r2, partials_out + (size_t)k * PARTIAL_BYTES);
+  }
   return BH_OK;
 }
 

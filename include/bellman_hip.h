@@ -161,6 +161,19 @@ bh_status bh_comm_init(bh_ctx* ctx, const uint8_t id[128], int nranks, int rank,
 /* all ranks' records, rank order: all_out holds nranks * BH_PARTIAL_BYTES bytes */
 bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t* all_out);
 bh_status bh_comm_destroy(bh_comm* c);
+/* This rank's partial record (rank/nranks from the communicator).  For nranks a power of two
+ * in [BH_DIST_H_MIN (default 4), 16] and m >= 2*nranks^2 the H block is distributed instead
+ * of replicated: every NTT is a local m/nranks-point NTT plus one ncclSend/ncclRecv
+ * all-to-all, three all-to-alls per proof, and this rank's h multiexp covers exactly the h
+ * coefficients it ends with (a strided set, not the range of bh_shard_range).  Otherwise
+ * identical to bh_prove_witness_partial(ctx, params, w, rank, nranks, ...). */
+bh_status bh_prove_witness_partial_comm(bh_ctx* ctx, const bh_params* params, const bh_witness* w, bh_comm* comm,
+                                        uint8_t partial_out[960]);
+/* All nshards partial records computed on this one device, the distributed H pipeline run
+ * with nshards virtual ranks and device copies for its all-to-alls (rehearsal and tests of
+ * the multi-GPU algorithm).  partials_out: nshards * BH_PARTIAL_BYTES. */
+bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, const bh_witness* w,
+                                          size_t nshards, uint8_t* partials_out);
 bh_status bh_ctx_synchronize(bh_ctx* ctx);
 int bh_device_count(void);
 

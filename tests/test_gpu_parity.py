@@ -400,6 +400,9 @@ def test_c4_2p24_sharded_8_ways_equals_single_device_proof():
         params.prepare(w, 8)
         parts = b"".join(bh.prove_witness_partial(c, params, w, k, 8) for k in range(8))
         assert bh.proof_from_partials(params.vk_bytes(), parts, 8, 27134, 17146) == single
+        # the same split with the H block distributed over the 8 (virtual) ranks
+        parts = bh.prove_witness_partials_local(c, params, w, 8)
+        assert bh.proof_from_partials(params.vk_bytes(), parts, 8, 27134, 17146) == single
         del params, w
     finally:
         c.close()
@@ -426,3 +429,18 @@ def test_device_proof_verifies_with_pairing(ctx, logc):
     image = cc.mimc(xl, xr, cc.fr_stream(7, rounds, bls.R), bls.R)
     assert pr.verify_proof(vk, proof, [image])
     assert not pr.verify_proof(vk, proof, [(image + 1) % bls.R])
+
+
+@pytest.mark.parametrize("logc,nshards", [(10, 2), (10, 4), (12, 8), (14, 16), (14, 4), (16, 8)])
+def test_distributed_h_partials_equal_single_proof(ctx, logc, nshards):
+    """The multi-GPU algorithm with the H block distributed (dist_h.h: per NTT a local
+    m/N-point NTT + one all-to-all + N-point DFTs; each rank's h multiexp over the strided
+    coefficient set it ends with), run with N virtual ranks on one device: the recombined
+    proof equals the single-device proof byte for byte."""
+    bh = _bh()
+    rounds = (1 << (logc - 1)) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    single = bh.prove_witness(ctx, params, w, 27134, 17146)
+    parts = bh.prove_witness_partials_local(ctx, params, w, nshards)
+    assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146) == single
