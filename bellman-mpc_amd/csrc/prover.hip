@@ -282,7 +282,12 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c) {
 bh_status prepare_tables(bh_ctx* ctx, bh_params* params, size_t m, size_t na, size_t a_aux_used, size_t b_aux_used,
                          size_t nshards) {
   if (!ctx->tables || ctx->window_override) return BH_OK;
-  const size_t N = std::max<size_t>(nshards, 1);
+  // BH_TABLE_C_FULL=1: window size chosen for the whole query, not the shard (A/B)
+  static const bool full_c = [] {
+    const char* e = getenv("BH_TABLE_C_FULL");
+    return e && e[0] == '1';
+  }();
+  const size_t N = full_c ? 1 : std::max<size_t>(nshards, 1);
   bh_status s;
   if ((s = ensure_table(ctx, &params->h, table_c_for((m - 1) / N)))) return s;
   if ((s = ensure_table(ctx, &params->l, table_c_for(na / N)))) return s;
@@ -486,16 +491,17 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
-    // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
-    const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
-    BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
-                              hipMemcpyDeviceToHost, st));
     return BH_OK;
   };
   auto tail_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
     BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + j], 0));
+    // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
+    // (copied here, off the accumulation stream)
+    const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
+    BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
+                              hipMemcpyDeviceToHost, st));
     if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out));
     else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out));
     return BH_OK;
@@ -542,7 +548,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
       if ((s = sort_job(big[q], sS))) return s;
     }
-    if ((s = run_small())) return s;
     BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
   } else {
     // the first sort is enqueued before the small multiexps: it gates the first accumulation
@@ -568,6 +573,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const int j = big[q];
     if ((s = acc_job(j, sA)) || (s = tail_job(j, tails[q]))) return s;
   }
+  // H first: the small multiexps are enqueued last (their ~50 launches would otherwise
+  // delay the host's enqueue of the first accumulation); they run in the shadow of the
+  // accumulations
+  if (h_first && (s = run_small())) return s;
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
   BH_TRY_HIP(hipStreamSynchronize(sH));

@@ -10,9 +10,11 @@ the complete assignment already resident in HBM; the output is the 192-byte
 proof.  Synthesis and CRS generation are outside the timed region.
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run): every MSM is
-sharded by scalar/point range over the N ranks; each rank returns its 8
-partial sums, RCCL all-gathers them (the one exchange step) and rank 0 adds
-them and assembles the proof.  Total work is fixed, so scaling is "strong".
+sharded by scalar/point range over the N ranks; for N >= 4 (power of two) the H
+block is distributed too (three RCCL all-to-alls per proof, dist_h.h) and each
+rank's h multiexp covers the coefficients it ends with.  Each rank returns its 8
+partial sums, RCCL all-gathers them and rank 0 adds them and assembles the
+proof.  Total work is fixed, so scaling is "strong".
 
 Prints ONE JSON line (rank 0).
 """
@@ -149,7 +151,10 @@ def main():
     def step():
         if world == 1:
             return bh.prove_witness(ctx, params, witness, r, s)
-        part = bh.prove_witness_partial(ctx, params, witness, rank, world)
+        if comm is not None:  # H block distributed over the ranks (RCCL all-to-alls) for N >= 4
+            part = comm.prove_partial(ctx, params, witness)
+        else:
+            part = bh.prove_witness_partial(ctx, params, witness, rank, world)
         if comm is not None:
             parts = comm.allgather(part)  # ncclAllGather over xGMI
         else:

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--shards", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--all-ranks", type=int, default=0, help="time every shard, not only shard 0 and N-1")
+    ap.add_argument("--local", type=int, default=0,
+                    help="also time bh_prove_witness_partials_local (all N ranks, distributed H emulated)")
     args = ap.parse_args()
     import bellman_hip as bh
     rounds = (1 << (args.log_constraints - 1)) - 1
@@ -44,6 +46,11 @@ def main():
             per[k] = round(min(ts), 3)
             worst = max(worst, min(ts))
         out["per_rank_ms"][n] = {"shards": per, "max": round(worst, 3)}
+        if args.local and n > 1:
+            bh.prove_witness_partials_local(ctx, params, w, n)  # warm-up
+            t0 = time.perf_counter()
+            bh.prove_witness_partials_local(ctx, params, w, n)
+            out.setdefault("local_all_ranks_ms", {})[n] = round((time.perf_counter() - t0) * 1e3, 3)
         print(json.dumps({"N": n, "per_rank_ms": per}), flush=True)
     base = out["per_rank_ms"].get(1, {}).get("max")
     if base:
