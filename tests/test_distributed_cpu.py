@@ -117,3 +117,105 @@ def test_shard_ranges_partition():
             spans = [bh.shard_range(n, k, N) for k in range(N)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[k][1] == spans[k + 1][0] for k in range(N - 1))
+
+
+# ---------------------------------------------------------------- distributed H (dist_h.hip)
+def _dist_h_share(a, b, c, N, rank, exchange):
+    """This rank's share {k: h[k]} of the H block computed as dist_h.hip does (three
+    all-to-alls, local M-point transforms, N-point DFTs); `exchange(blocks)` sends
+    blocks[p] to rank p and returns the blocks received, indexed by source rank."""
+    from oracle import bls12_381 as bls
+    q = bls.R
+    m = len(a)
+    L = m.bit_length() - 1
+    M, C = m // N, m // N // N
+    w = pow(bls.FR_ROOT_OF_UNITY, 1 << (32 - L), q)
+    wi = pow(w, q - 2, q)
+    wN, wNi = pow(w, M, q), pow(wi, M, q)
+    g, gi = 7, pow(7, q - 2, q)
+    minv = pow(m, q - 2, q)
+    zinv = pow((pow(g, m, q) - 1) % q, q - 2, q)
+
+    def dft(x, root):
+        n = len(x)
+        return [sum(x[j] * pow(root, j * k, q) for j in range(n)) % q for k in range(n)]
+
+    # phase 1: residue class r, local inverse M-point NTT (root w^-N)
+    Y = [dft([v[N * j + rank] for j in range(M)], pow(wi, N, q)) for v in (a, b, c)]
+    got = exchange([[y[p * C:(p + 1) * C] for y in Y] for p in range(N)])
+    # phase 2: inverse N-DFT over sources (twiddle w^-qr), coset scale, forward N-DFT (w^qr)
+    rows = [[[0] * C for _ in range(3)] for _ in range(N)]
+    for vi in range(3):
+        for u in range(C):
+            qq = rank * C + u
+            R = [got[r][vi][u] * pow(wi, qq * r, q) % q for r in range(N)]
+            X = dft(R, wNi)
+            X = [X[t] * pow(g, t * M + qq, q) * minv % q for t in range(N)]
+            Wv = dft(X, wN)
+            for r2 in range(N):
+                rows[r2][vi][u] = Wv[r2] * pow(w, qq * r2, q) % q
+    got = exchange(rows)
+    V = [sum((got[src][vi] for src in range(N)), []) for vi in range(3)]  # natural q
+    # phase 3: forward M-point NTTs (root w^N), a*b - c, / Z(g), inverse M-point NTT
+    Fa, Fb, Fc = (dft(v, pow(w, N, q)) for v in V)
+    hc = [(Fa[j] * Fb[j] - Fc[j]) * zinv % q for j in range(M)]
+    Yh = dft(hc, pow(wi, N, q))
+    got = exchange([[Yh[p * C:(p + 1) * C]] for p in range(N)])
+    # final: inverse N-DFT over sources, icoset scale
+    share = {}
+    for u in range(C):
+        qq = rank * C + u
+        R = [got[r][0][u] * pow(wi, qq * r, q) % q for r in range(N)]
+        X = dft(R, wNi)
+        for t in range(N):
+            k = t * M + qq
+            share[k] = X[t] * pow(gi, k, q) * minv % q
+    return share
+
+
+def _dist_h_worker(rank, world, port, q):
+    import random
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import bls12_381 as bls
+    rng = random.Random(1234)
+    m = 64
+    a, b, c = ([rng.randrange(bls.R) for _ in range(m)] for _ in range(3))
+
+    def exchange(blocks):
+        allb = [None] * world
+        dist.all_gather_object(allb, blocks)
+        return [allb[src][rank] for src in range(world)]
+
+    share = _dist_h_share(a, b, c, world, rank, exchange)
+    shares = [None] * world
+    dist.all_gather_object(shares, share)
+    if rank == 0:
+        from oracle import bellman as bm
+        want = bm.compute_h(bm.BLS12_381, a, b, c)
+        merged = {}
+        for s in shares:
+            assert not set(s) & set(merged)
+            merged.update(s)
+        q.put(sorted(merged) == list(range(m)) and [merged[k] for k in range(m - 1)] == want)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_distributed_h_gloo(world):
+    """The distributed H block (dist_h.hip's index algebra and exchange pattern) with `world`
+    gloo ranks: the union of the ranks' shares is the oracle's H (prover.rs:210-231)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dist_h_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    ok = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+    assert ok
+    assert all(p.exitcode == 0 for p in procs)
