@@ -589,7 +589,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
   if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->host_counts, 16 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     delete c;
     return BH_ERR_OUT_OF_MEMORY;
   }

@@ -126,7 +126,9 @@ struct bh_ctx {
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
   double last_timings[10] = {};
-  uint32_t* host_counts = nullptr;  // pinned: entries (= mixed additions) of each prover multiexp
+  uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp,
+                                    // [16,32) its continuation span (max_span)
+  bh::DevBuf dspan;                 // device words for max_span
   std::mutex mu;
 };
 

@@ -66,10 +66,18 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
 template <class C>
 hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
                      size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh, MsmTiming* timing);
+// max_span: the largest number of continuation partials of one bucket (max_span() below)
+// when known, so that only the continuation-tree levels that can do work are launched;
+// -1: every level a bucket could need
 template <class C>
-hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out);
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
+                    int max_span = -1);
 
 size_t scan_scratch_words(size_t n);
+// max over buckets of (last segment - first segment) for segment length S, into d_word and
+// (pinned) *h_word, stream-ordered: the continuation-tree depth msm_back needs
+hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_word,
+                    uint32_t* h_word, hipStream_t st);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st);
 hipError_t scalars_prepare(const uint32_t* d_in, uint32_t* d_out, size_t n, int mode, int log_perm, hipStream_t st);
 hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset, int32_t* d_idx, uint32_t* d_tmp,

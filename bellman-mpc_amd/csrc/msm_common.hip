@@ -384,6 +384,31 @@ hipError_t scalars_prepare(const uint32_t* d_in, uint32_t* d_out, size_t n, int 
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) k_max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt,
+                                                  uint32_t S, uint32_t* out) {
+  uint32_t m = 0;
+  for (size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x; b < nbt; b += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t cnt = counts[b];
+    if (cnt) {
+      const uint32_t off = offsets[b];
+      m = max(m, (off + cnt - 1) / S - off / S);
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_word,
+                    uint32_t* h_word, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(d_word, 0, 4, st);
+  if (e != hipSuccess) return e;
+  const unsigned g = (unsigned)std::min<size_t>(1024, (nbt + 255) / 256);
+  hipLaunchKernelGGL(k_max_span, dim3(std::max(1u, g)), dim3(256), 0, st, counts, offsets, nbt, S, d_word);
+  if (h_word) e = hipMemcpyAsync(h_word, d_word, 4, hipMemcpyDeviceToHost, st);
+  return e != hipSuccess ? e : hipGetLastError();
+}
+
 hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset, int32_t* d_idx, uint32_t* d_tmp,
                          uint32_t* d_scan_scratch, hipStream_t st) {
   const size_t nwords = (n + 63) / 64;

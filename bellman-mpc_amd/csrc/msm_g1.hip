@@ -12,5 +12,5 @@ template hipError_t msm_accumulate<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, con
                                            MsmTiming*);
 template hipError_t msm_front<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
-template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, size_t, const MsmShape&, typename G1Ops::P*);
+template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, size_t, const MsmShape&, typename G1Ops::P*, int);
 }  // namespace bh

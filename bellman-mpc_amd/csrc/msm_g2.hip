@@ -12,5 +12,5 @@ template hipError_t msm_accumulate<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, con
                                            MsmTiming*);
 template hipError_t msm_front<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
-template hipError_t msm_back<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, size_t, const MsmShape&, typename G2Ops::P*);
+template hipError_t msm_back<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, size_t, const MsmShape&, typename G2Ops::P*, int);
 }  // namespace bh

@@ -460,11 +460,13 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 
 // Back half: continuation fix-up, summation by parts and the per-window sums, copied to host_out (W entries).
 template <class C>
-hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out) {
+hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
+                    int max_span) {
   const size_t nbt = (size_t)sh.Wb * sh.NB;
   // log-depth continuation fix-up: a bucket can span up to segs segments
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
-  for (int level = 0; ((size_t)1 << level) < segs; level++)
+  const size_t span = max_span >= 0 ? (size_t)max_span : segs;
+  for (int level = 0; ((size_t)1 << level) < span; level++)
     hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
                        ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   const uint32_t T = (uint32_t)(sh.NB / sh.L);

@@ -320,6 +320,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(ctx->idx.alloc(maxn * 4));
   BH_TRY_HIP(ctx->dtmp.alloc((maxn / 64 + 2) * 4));
   BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(maxn / 64 + 2) * 4 + 64));
+  BH_TRY_HIP(ctx->dspan.alloc(16 * 4));
 
   if ((s = prepare_tables(ctx, const_cast<bh_params*>(params), m, na, w->a_aux_total, w->b_aux_total, nshards)))
     return s;
@@ -350,7 +351,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   // Streams, all ordered after whatever ran before on ctx->stream:
   //   stream    : the bucket accumulations back to back (VALU-bound critical path);
-  //   stream4   : the H pipeline (by default alone at the start, see h_first below);
+  //   stream4   : the H pipeline (after the first accumulation, or first when distributed);
   //   stream3   : density maps, then every multiexp's sort (memory-bound, runs ahead);
   //   stream2   : the small (public-input) multiexps, whole;
   //   tstream[q]: the reduction tail of the q-th large multiexp.
@@ -470,13 +471,55 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     hipEventRecord(ctx->ev[1], sH);
     return BH_OK;
   };
+  // Two multiexps with the same scalars, density map, range and digit geometry (b_g1_aux and
+  // b_g2_aux: prover.rs:282-307 both use the aux assignment under b_aux_density) have
+  // identical sorted entries, so the second one copies the first one's instead of sorting.
+  auto same_digits = [&](int i, int j) {
+    const MsmShape &a = shapes[i], &b = shapes[j];
+    return jobs[i].sc == jobs[j].sc && jobs[i].idx == jobs[j].idx && los[i] == los[j] && his[i] == his[j] &&
+           a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre;
+  };
+  int sorted_from[8];
+  for (int j = 0; j < 8; j++) sorted_from[j] = -1;
   auto sort_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
     const int32_t* ix = J.idx ? J.idx + los[j] : nullptr;
     const uint32_t* sc = J.sc + los[j] * 8;
-    if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
-    else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
+    int src = -1;
+    for (int i = 0; i < 8 && src < 0; i++)
+      if (i != j && sorted_from[i] == i && same_digits(i, j)) src = i;
+    if (src >= 0) {
+      const MsmShape& sh = shapes[j];
+      const size_t nbt = (size_t)sh.Wb * sh.NB;
+      const uint32_t *e, *cn, *of;
+      if (jobs[src].g2) { e = ctx->pw2[jobs[src].out].entries; cn = ctx->pw2[jobs[src].out].counts; of = ctx->pw2[jobs[src].out].offsets; }
+      else { e = ctx->pw1[jobs[src].out].entries; cn = ctx->pw1[jobs[src].out].counts; of = ctx->pw1[jobs[src].out].offsets; }
+      uint32_t *de, *dc, *dof;
+      if (J.g2) {
+        BH_TRY_HIP(ctx->pw2[J.out].reserve_shape(n, sh));
+        de = ctx->pw2[J.out].entries; dc = ctx->pw2[J.out].counts; dof = ctx->pw2[J.out].offsets;
+      } else {
+        BH_TRY_HIP(ctx->pw1[J.out].reserve_shape(n, sh));
+        de = ctx->pw1[J.out].entries; dc = ctx->pw1[J.out].counts; dof = ctx->pw1[J.out].offsets;
+      }
+      BH_TRY_HIP(hipStreamWaitEvent(st, jev[16 + src], 0));
+      BH_TRY_HIP(hipMemcpyAsync(dc, cn, (nbt + 1) * 4, hipMemcpyDeviceToDevice, st));
+      BH_TRY_HIP(hipMemcpyAsync(dof, of, (nbt + 1) * 4, hipMemcpyDeviceToDevice, st));
+      BH_TRY_HIP(hipMemcpyAsync(de, e, n * (size_t)sh.W * 4, hipMemcpyDeviceToDevice, st));
+      sorted_from[j] = src;
+    } else {
+      if (J.g2) BH_TRY_HIP(msm_sort<G2Ops>(ctx->pw2[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
+      else BH_TRY_HIP(msm_sort<G1Ops>(ctx->pw1[J.out], st, sc, n, ix, (uint32_t)los[j], shapes[j]));
+      sorted_from[j] = j;
+    }
+    // continuation-tree depth of this multiexp (read by its tail, so it launches only the
+    // levels that can do work)
+    const MsmShape& shj = shapes[j];
+    const uint32_t* cnt = J.g2 ? ctx->pw2[J.out].counts : ctx->pw1[J.out].counts;
+    const uint32_t* off = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
+    BH_TRY_HIP(max_span(cnt, off, (size_t)shj.Wb * shj.NB, (uint32_t)shj.S, ctx->dspan.as<uint32_t>() + j,
+                        ctx->host_counts + 16 + j, st));
     BH_TRY_HIP(hipEventRecord(jev[16 + j], st));
     return BH_OK;
   };
@@ -502,8 +545,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
     BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
                               hipMemcpyDeviceToHost, st));
-    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out));
-    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out));
+    int span = -1;
+    if (n >= SMALL_JOB) {  // the sort ran ahead; its span word is on the host once it is done
+      BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
+      span = (int)ctx->host_counts[16 + j];
+    }
+    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span));
+    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span));
     return BH_OK;
   };
   BH_TRY_HIP(hipEventRecord(jev[33], sS));
@@ -521,15 +569,17 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   int h_pos = nbig;
   for (int q = 0; q < nbig; q++)
     if (jobs[big[q]].is_h) h_pos = q;
-  // H first (default): the pipeline runs alone at the start, next to the memory-bound sorts,
-  // and the first accumulation waits for it.  Run concurrently with an accumulation, its
-  // short NTT passes only get CUs as accumulation workgroups retire (stream priority does
-  // not change that) and it stretches from ~5 ms to ~30 ms, leaving h's accumulation waiting.
-  // BH_H_FIRST=0: H after the first accumulation, overlapped (A/B experiments).
-  static const bool h_first = [] {
+  // H placement.  Replicated H (one GPU, or N < BH_DIST_H_MIN): H starts after the first
+  // accumulation and overlaps the next ones (its NTT passes only get CUs as accumulation
+  // workgroups retire, so it stretches to ~25 ms, but h's accumulation is the last one and
+  // the H work fills the accumulations' gaps; measured ~1.5 ms faster than running it first).
+  // Distributed H: first, next to the sorts, so its RCCL all-to-alls never wait behind a
+  // whole-GPU accumulation.  BH_H_FIRST=0/1 forces either (A/B experiments).
+  static const int h_first_env = [] {
     const char* e = getenv("BH_H_FIRST");
-    return !(e && e[0] == '0');
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
   }();
+  const bool h_first = h_first_env >= 0 ? h_first_env == 1 : dh != nullptr;
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -541,7 +591,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     }
     return BH_OK;
   };
-  int next_acc = 0;
+  // Host enqueue order follows the critical path: the first sort and accumulation, H, the
+  // remaining sorts (h's after H), every accumulation, then the tails and the small
+  // multiexps, whose ~200 short launches would otherwise delay the accumulations' enqueue.
   if (h_first) {
     if ((s = enqueue_h(jev[33]))) return s;
     for (int q = 0; q < nbig; q++) {
@@ -549,34 +601,27 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if ((s = sort_job(big[q], sS))) return s;
     }
     BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
+    for (int q = 0; q < nbig; q++)
+      if ((s = acc_job(big[q], sA))) return s;
   } else {
-    // the first sort is enqueued before the small multiexps: it gates the first accumulation
-    for (int q = 0; q < h_pos; q++) {
-      if ((s = sort_job(big[q], sS))) return s;
-      if (q == 0 && (s = run_small())) return s;
-    }
-    if (h_pos == 0 && (s = run_small())) return s;
+    int q0 = 0;
     if (h_pos > 0) {
-      if ((s = acc_job(big[0], sA))) return s;
-      if ((s = enqueue_h(jev[24 + big[0]]))) return s;  // ahead of the first tail on its stream
-      if ((s = tail_job(big[0], tails[0]))) return s;
-      next_acc = 1;
+      if ((s = sort_job(big[0], sS)) || (s = acc_job(big[0], sA))) return s;
+      if ((s = enqueue_h(jev[24 + big[0]]))) return s;
+      q0 = 1;
     } else if ((s = enqueue_h(jev[33]))) {
       return s;
     }
-    for (int q = h_pos; q < nbig; q++) {
+    for (int q = q0; q < nbig; q++) {
       if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
       if ((s = sort_job(big[q], sS))) return s;
     }
+    for (int q = q0; q < nbig; q++)
+      if ((s = acc_job(big[q], sA))) return s;
   }
-  for (int q = next_acc; q < nbig; q++) {
-    const int j = big[q];
-    if ((s = acc_job(j, sA)) || (s = tail_job(j, tails[q]))) return s;
-  }
-  // H first: the small multiexps are enqueued last (their ~50 launches would otherwise
-  // delay the host's enqueue of the first accumulation); they run in the shadow of the
-  // accumulations
-  if (h_first && (s = run_small())) return s;
+  for (int q = 0; q < nbig; q++)
+    if ((s = tail_job(big[q], tails[q]))) return s;
+  if ((s = run_small())) return s;
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
   BH_TRY_HIP(hipStreamSynchronize(sH));
