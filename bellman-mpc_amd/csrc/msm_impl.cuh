@@ -96,12 +96,14 @@ __global__ void __launch_bounds__(256) k_cont_tree(const uint32_t* cont_bucket, 
   store_point<C>(&conts[s], C::add(load_point<C>(&conts[s]), load_point<C>(&conts[s + half])));
 }
 
-// thread (w, t): buckets [t*L, (t+1)*L) of window w
+// Bucket reduction: thread (w, t) sums its L buckets by parts
+// (multiexp.rs:229-233 restricted to buckets [t*L, (t+1)*L)) and adds (t*L) * (their sum),
+// so out[w*T + t] = sum_{k<L} (t*L + k + 1) * B[t*L + k]  (bucket b holds digit b+1)
 template <class C>
-__global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t* counts, const uint32_t* offsets,
+__global__ void __launch_bounds__(64) k_bucket_combine(const uint32_t* counts, const uint32_t* offsets,
                                                        const typename C::P* bucket_sums, const typename C::P* conts,
                                                        uint32_t S, uint32_t NB, uint32_t L, uint32_t W,
-                                                       typename C::P* seg_weighted, typename C::P* seg_sum) {
+                                                       typename C::P* out) {
   const uint32_t T = NB / L;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= W * T) return;
@@ -112,45 +114,45 @@ __global__ void __launch_bounds__(256) k_bucket_reduce(const uint32_t* counts, c
     running = C::add(running, bucket_value<C>(gb, counts, offsets, bucket_sums, conts, S));
     acc = C::add(acc, running);
   }
-  store_point<C>(&seg_weighted[gid], acc);
-  store_point<C>(&seg_sum[gid], running);
-}
-
-// v_t = weighted_t + (t*L) * sum_t
-template <class C>
-__global__ void __launch_bounds__(256) k_seg_combine(typename C::P* seg_weighted, const typename C::P* seg_sum,
-                                                     uint32_t T, uint32_t L, uint32_t total) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const uint32_t k = (gid % T) * L;
-  typename C::P v = load_point<C>(&seg_weighted[gid]);
+  const uint32_t k = t * L;
   if (k != 0) {
-    const typename C::P base = load_point<C>(&seg_sum[gid]);
     typename C::P m = C::identity();
     for (int bit = 31 - __clz(k); bit >= 0; bit--) {
       m = C::dbl(m);
-      if ((k >> bit) & 1u) m = C::add(m, base);
+      if ((k >> bit) & 1u) m = C::add(m, running);
     }
-    v = C::add(v, m);
+    acc = C::add(acc, m);
   }
-  store_point<C>(&seg_weighted[gid], v);
+  store_point<C>(&out[gid], acc);
 }
 
-// one level of the per-window sum: out[w][t] = sum of in[w][t*G .. t*G+G) (G <= 4 keeps the
-// sequential chain short; the tail of the last multiexp is latency-bound).  The last level
-// (Tout == 1) writes canonical coordinates.
+// Block-level sum: block (w, g) adds in[w][g*4B .. g*4B+4B) (B = blockDim: four points per
+// thread, then a B-way tree in LDS; B*sizeof(P) = 56 KB for G1 at B = 256, G2 at B = 128) into
+// out[w*Tout + g].  Two launches reduce up to 2^18 (G1) points.  With Tout == 1 the result is
+// written in canonical coordinates.
 template <class C>
-__global__ void __launch_bounds__(64) k_sum_groups(const typename C::P* in, uint32_t Tin, uint32_t G,
-                                                   typename C::P* out, uint32_t Tout, uint32_t W) {
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= W * Tout) return;
-  const uint32_t w = gid / Tout, t = gid % Tout;
+__global__ void __launch_bounds__(256) k_sum_tree(const typename C::P* in, uint32_t Tin, typename C::P* out,
+                                                  uint32_t Tout) {
+  extern __shared__ uint4 lds_raw[];
+  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  const uint32_t w = blockIdx.x / Tout, g = blockIdx.x % Tout;
   const typename C::P* src = in + (size_t)w * Tin;
-  const uint32_t lo = t * G, hi = min(lo + G, Tin);
-  typename C::P acc = load_point<C>(&src[lo]);
-  for (uint32_t i = lo + 1; i < hi; i++) acc = C::add(acc, load_point<C>(&src[i]));
-  if (Tout == 1) out[w] = C::reduce(acc);
-  else store_point<C>(&out[gid], acc);
+  const uint32_t lo = g * 4u * blockDim.x + threadIdx.x * 4u;
+  typename C::P acc = C::identity();
+  for (uint32_t i = lo; i < min(lo + 4u, Tin); i++) acc = C::add(acc, load_point<C>(&src[i]));
+  store_point<C>(&lds[threadIdx.x], acc);
+  __syncthreads();
+  for (uint32_t h = blockDim.x / 2; h > 0; h >>= 1) {
+    if (threadIdx.x < h) {
+      acc = C::add(acc, load_point<C>(&lds[threadIdx.x + h]));
+      store_point<C>(&lds[threadIdx.x], acc);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (Tout == 1) out[w] = C::reduce(acc);
+    else store_point<C>(&out[(size_t)w * Tout + g], acc);
+  }
 }
 
 // The accumulate kernel needs E; it reads it from offsets[nbt] on device.
@@ -471,19 +473,18 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
                        ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
   const size_t total = (size_t)sh.Wb * T;
-  hipLaunchKernelGGL(k_bucket_reduce<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
+  hipLaunchKernelGGL(k_bucket_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
                      ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, (uint32_t)sh.L, (uint32_t)sh.Wb,
-                     ws.seg_weighted, ws.seg_sum);
-  hipLaunchKernelGGL(k_seg_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.seg_weighted, ws.seg_sum, T,
-                     (uint32_t)sh.L, (uint32_t)total);
-  // seg_weighted -> seg_sum -> seg_weighted ... -> window_sums
+                     ws.seg_weighted);
+  // seg_weighted -> seg_sum -> seg_weighted ... -> window_sums, 4*B points per block per level
+  constexpr uint32_t B = sizeof(typename C::P) > 256 ? 128 : 256;
   typename C::P* bufs[2] = {ws.seg_weighted, ws.seg_sum};
   uint32_t Tin = T;
   for (int lvl = 0;; lvl++) {
-    const uint32_t Tout = (Tin + 3) / 4;
+    const uint32_t Tout = (Tin + 4 * B - 1) / (4 * B);
     typename C::P* dst = Tout == 1 ? ws.window_sums : bufs[(lvl + 1) & 1];
-    hipLaunchKernelGGL(k_sum_groups<C>, dim3(msm_blocks_for((size_t)sh.Wb * Tout, 64)), dim3(64), 0, st, bufs[lvl & 1],
-                       Tin, 4u, dst, Tout, (uint32_t)sh.Wb);
+    hipLaunchKernelGGL(k_sum_tree<C>, dim3((unsigned)(sh.Wb * Tout)), dim3(B), B * sizeof(typename C::P), st,
+                       bufs[lvl & 1], Tin, dst, Tout);
     if (Tout == 1) break;
     Tin = Tout;
   }
