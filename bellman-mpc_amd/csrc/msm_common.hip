@@ -194,7 +194,9 @@ MsmShape msm_shape(size_t n, int c_override) {
   sh.c = c;
   sh.W = (256 + c - 1) / c;
   sh.NB = 1 << (c - 1);
-  sh.L = std::min<int>(8, sh.NB);
+  // buckets per reduction thread: 8 for large bucket sets (less segment-combine work), 4 below
+  // 2^18 buckets (more threads, shorter chains: the tail of a small shard is latency-bound)
+  sh.L = std::min<int>(sh.NB >= (1 << 18) ? 8 : 4, sh.NB);
   size_t E = n * (size_t)sh.W;
   int S = 16;
   while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;

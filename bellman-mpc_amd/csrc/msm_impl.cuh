@@ -96,6 +96,24 @@ __global__ void __launch_bounds__(256) k_cont_tree(const uint32_t* cont_bucket, 
   store_point<C>(&conts[s], C::add(load_point<C>(&conts[s]), load_point<C>(&conts[s + half])));
 }
 
+// The same fold for buckets spanning at most CONT_SEQ_MAX segments, one thread per bucket:
+// conts[s_first+1] += conts[s_first+2] + ... + conts[s_last]
+constexpr size_t CONT_SEQ_MAX = 24;
+template <class C>
+__global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t nbt,
+                                                  uint32_t S, typename C::P* conts) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbt) return;
+  const uint32_t cnt = counts[b];
+  if (cnt == 0) return;
+  const uint32_t off = offsets[b];
+  const uint32_t s_first = off / S, s_last = (off + cnt - 1) / S;
+  if (s_last < s_first + 2) return;
+  typename C::P acc = load_point<C>(&conts[s_first + 1]);
+  for (uint32_t sg = s_first + 2; sg <= s_last; sg++) acc = C::add(acc, load_point<C>(&conts[sg]));
+  store_point<C>(&conts[s_first + 1], acc);
+}
+
 // Bucket reduction: thread (w, t) sums its L buckets by parts
 // (multiexp.rs:229-233 restricted to buckets [t*L, (t+1)*L)) and adds (t*L) * (their sum),
 // so out[w*T + t] = sum_{k<L} (t*L + k + 1) * B[t*L + k]  (bucket b holds digit b+1)
@@ -468,9 +486,17 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   // log-depth continuation fix-up: a bucket can span up to segs segments
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
-  for (int level = 0; ((size_t)1 << level) < span; level++)
-    hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket, ws.counts,
-                       ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
+  if (max_span >= 0 && span <= CONT_SEQ_MAX) {
+    // short spans (the common case, known from the sort): one thread per bucket folds its
+    // continuation partials in sequence -- one launch instead of log2(span) full-grid levels
+    if (span >= 2)
+      hipLaunchKernelGGL(k_cont_seq<C>, dim3(msm_blocks_for(nbt, 256)), dim3(256), 0, st, ws.counts, ws.offsets,
+                         (uint32_t)nbt, (uint32_t)sh.S, ws.conts);
+  } else {
+    for (int level = 0; ((size_t)1 << level) < span; level++)
+      hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
+                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
+  }
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
   const size_t total = (size_t)sh.Wb * T;
   hipLaunchKernelGGL(k_bucket_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
