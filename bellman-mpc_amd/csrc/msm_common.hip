@@ -210,11 +210,17 @@ MsmShape msm_shape(size_t n, int c_override) {
 // With a window table every digit window adds into one shared set of 2^(c-1) buckets, so
 // the accumulation costs n*ceil(256/c) mixed additions and the reduction ~6.5 * 2^(c-1)
 // (2 running-sum additions per bucket plus the segment combine), independent of W.
+// Only window sizes whose top window holds >= 10 real scalar bits: with shared buckets a
+// nearly empty top window (e.g. c = 17: the 16th window only takes the carry; c = 18: 3 bits)
+// pours up to n/2 entries into a handful of small-digit buckets, whose continuation partials
+// then need the log-depth tree (msm_back).  For 255-bit scalars: c = 16, 20, 22, 24.
 int msm_table_c(size_t n) {
   int best = 16;
   double best_cost = 1e300;
-  for (int c = 8; c <= 22; c++) {
-    const double cost = (double)n * ((256 + c - 1) / c) + 6.5 * (double)((size_t)1 << (c - 1));
+  for (int c = 8; c <= 24; c++) {
+    const int W = (256 + c - 1) / c;
+    if (255 - (W - 1) * c < 10) continue;
+    const double cost = (double)n * W + 6.5 * (double)((size_t)1 << (c - 1));
     if (cost < best_cost) { best_cost = cost; best = c; }
   }
   return best;
