@@ -83,13 +83,14 @@ struct CurveOps {
     T M = F::add(F::add(xx, xx), xx);
     P r;
     r.X = F::template sub<K1>(F::sqr(M), F::add(S, S));
-    r.Y = F::template sub<K3>(F::mul(M, F::template sub<K2>(S, r.X)), F::mul(W, p.Y));
+    r.Y = F::template mul_sub<KY>(M, F::template sub<K2>(S, r.X), p.Y, W);
     r.ZZ = F::mul(V, p.ZZ);
     r.ZZZ = F::mul(W, p.ZZZ);
     return r;
   }
 
-  // p + a, a affine and not the identity (madd-2008-s)
+  // p + a, a affine and not the identity (madd-2008-s); Y3 = R(Q - X3) - Y1*PPP with one
+  // Montgomery reduction for both products over Fp (F::mul_sub)
   static BH_DEV P madd(const P& p, const A& a) {
     if (is_identity(p)) return from_affine(a);
     T U2 = F::mul(a.x, p.ZZ);
@@ -105,7 +106,7 @@ struct CurveOps {
     T Q = F::mul(p.X, PP);
     P r;
     r.X = F::template sub<K1>(F::sqr(R), F::add(PPP, F::add(Q, Q)));
-    r.Y = F::template sub<K3>(F::mul(R, F::template sub<K2>(Q, r.X)), F::mul(p.Y, PPP));
+    r.Y = F::template mul_sub<KY>(R, F::template sub<K2>(Q, r.X), p.Y, PPP);
     r.ZZ = F::mul(p.ZZ, PP);
     r.ZZZ = F::mul(p.ZZZ, PPP);
     return r;
@@ -130,7 +131,7 @@ struct CurveOps {
     T Q = F::mul(U1, PP);
     P r;
     r.X = F::template sub<K1>(F::sqr(R), F::add(PPP, F::add(Q, Q)));
-    r.Y = F::template sub<K3>(F::mul(R, F::template sub<K2>(Q, r.X)), F::mul(S1, PPP));
+    r.Y = F::template mul_sub<K3>(R, F::template sub<K2>(Q, r.X), S1, PPP);
     r.ZZ = F::mul(F::mul(p.ZZ, q.ZZ), PP);
     r.ZZZ = F::mul(F::mul(p.ZZZ, q.ZZZ), PPP);
     return r;

@@ -90,6 +90,39 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
   return r;
 }
 
+// (a*b + c*d) * R^-1 with ONE interleaved Montgomery reduction: every column absorbs the
+// products of both pairs and the m*p terms -- at most 3N = 42 products < 2^58 each for DFp,
+// so the 64-bit accumulator still needs no carry handling (2^63.4).  Output < 2p when the
+// operand bounds (in multiples of p) satisfy A*B + C*D < R/p (2^25 for DFp).
+template <class C>
+BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+  constexpr int N = C::N;
+  static_assert(3 * N < 64, "3N products < 2^58 plus the carry must fit the 64-bit column accumulator");
+  Fe<C> r;
+  uint32_t m[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acc += (uint64_t)c.v[i] * d.v[k - i];
+    }
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
+      acc += (uint64_t)m[i] * C::P[k - i];
+    if (k < N) {
+      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      acc += (uint64_t)m[k] * C::P[0];
+    } else {
+      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+    }
+    acc >>= BH_LIMB_BITS;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  return r;
+}
+
 // Montgomery square: cross products computed once against 2*a (limbs < 2^30).
 template <class C>
 BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
@@ -280,6 +313,10 @@ struct FpOps {
   static BH_DEV T sqr(const T& a) { return fe_sqr<FpCfg>(a); }
   static BH_DEV T add(const T& a, const T& b) { return fe_add<FpCfg>(a, b); }
   template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) { return fe_sub<FpCfg, K>(a, b); }
+  // a*b - c*d with c < K*p: one reduction for both products (fe_mul2 of a, b, K*p - c, d); < 2p
+  template <uint32_t K> static BH_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
+    return fe_mul2<FpCfg>(a, b, fe_neg<FpCfg, K>(c), d);
+  }
   static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a); }
   static BH_DEV T zero() { return fe_zero<FpCfg>(); }
   static BH_DEV T one() { return fe_one<FpCfg>(); }
@@ -292,6 +329,12 @@ struct FpOps {
   static BH_DEV T unpack(const uint32_t* w) { return fe_unpack<FpCfg>(w); }
   static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<FpCfg>(a, w); }
 };
+
+constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
+  uint32_t r = 1;
+  while (r < x) r <<= 1;
+  return r;
+}
 
 struct Fp2Ops {
   using T = DFp2;
@@ -318,6 +361,10 @@ struct Fp2Ops {
   }
   template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) {
     return T{fe_sub<FpCfg, K>(a.c0, b.c0), fe_sub<FpCfg, K>(a.c1, b.c1)};
+  }
+  // a*b - c*d (c unused as a bound here: both products are reduced, < MB*p each)
+  template <uint32_t K> static BH_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
+    return sub<bh_pow2_ceil_fp2(MB)>(mul(a, b), mul(c, d));
   }
   static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a.c0) && fe_is_zero<FpCfg>(a.c1); }
   static BH_DEV T zero() { return T{fe_zero<FpCfg>(), fe_zero<FpCfg>()}; }
