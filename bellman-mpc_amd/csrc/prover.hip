@@ -1,5 +1,6 @@
 // Groth16 prover core on the device: Parameters handling (groth16/mod.rs:224-477)
 // and create_proof after synthesis (groth16/prover.rs:206-349).
+#include <stdio.h>
 #include <string.h>
 
 #include <chrono>
@@ -410,13 +411,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     hjob = Job{false, &params->h, hshare->hbuf.as<uint32_t>(), hshare->M, hshare->hidx.as<int32_t>(), used, 0, true,
                true};
   }
-  // G2 first (the longest tail gets the most overlap), h last so the H pipeline has three
-  // accumulations of slack
+  // G2 first (the longest tail gets the most overlap), then b_g1_aux whose sorted digits are
+  // a copy of b_g2_aux's (so both are ready at the first accumulation for the price of one
+  // sort), h last so the H pipeline has the most slack
   const Job jobs[8] = {
       {true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1},              // b_g2_aux
+      {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
       {false, &params->l, aux, na, nullptr, na, 1},                             // l
       {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
-      {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
       hjob,                                                                     // h
       {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
       {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
@@ -569,17 +571,16 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   int h_pos = nbig;
   for (int q = 0; q < nbig; q++)
     if (jobs[big[q]].is_h) h_pos = q;
-  // H placement.  Replicated H (one GPU, or N < BH_DIST_H_MIN): H starts after the first
-  // accumulation and overlaps the next ones (its NTT passes only get CUs as accumulation
-  // workgroups retire, so it stretches to ~25 ms, but h's accumulation is the last one and
-  // the H work fills the accumulations' gaps; measured ~1.5 ms faster than running it first).
-  // Distributed H: first, next to the sorts, so its RCCL all-to-alls never wait behind a
-  // whole-GPU accumulation.  BH_H_FIRST=0/1 forces either (A/B experiments).
-  static const int h_first_env = [] {
-    const char* e = getenv("BH_H_FIRST");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it (the
+  // distributed default: its RCCL all-to-alls never wait behind a whole-GPU accumulation);
+  // 1 = from the start, concurrent with everything; 2 = after the first accumulation (the
+  // replicated default: H's ~4.5 ms of NTT work fills the later accumulations' round
+  // boundaries and is done before h, accumulated last; ~1 ms faster than 1 at 2^22).
+  static const int h_mode_env = [] {
+    const char* e = getenv("BH_H_MODE");
+    return e ? atoi(e) : -1;
   }();
-  const bool h_first = h_first_env >= 0 ? h_first_env == 1 : dh != nullptr;
+  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 0 : 2);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -591,42 +592,42 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     }
     return BH_OK;
   };
-  // Host enqueue order follows the critical path: the first sort and accumulation, H, the
-  // remaining sorts (h's after H), every accumulation, then the tails and the small
-  // multiexps, whose ~200 short launches would otherwise delay the accumulations' enqueue.
-  if (h_first) {
+  // Host enqueue order follows the critical path: the first two sorts (a sort running beside
+  // a whole-GPU accumulation only gets CUs as its workgroups retire, so the second one would
+  // not be ready when the first accumulation ends), the first accumulation, H, the remaining
+  // sorts (h's after H), every accumulation, the small multiexps, then the tails.
+  const int pre_sorts = std::min(nbig, h_pos == 1 ? 1 : 2);
+  if (h_pos < pre_sorts && h_mode == 2) h_mode = 1;  // h's own sort is among the first: H first
+  if (h_mode == 0 || h_mode == 1) {
     if ((s = enqueue_h(jev[33]))) return s;
-    for (int q = 0; q < nbig; q++) {
-      if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-      if ((s = sort_job(big[q], sS))) return s;
-    }
-    BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
-    for (int q = 0; q < nbig; q++)
-      if ((s = acc_job(big[q], sA))) return s;
-  } else {
-    int q0 = 0;
-    if (h_pos > 0) {
-      if ((s = sort_job(big[0], sS)) || (s = acc_job(big[0], sA))) return s;
-      if ((s = enqueue_h(jev[24 + big[0]]))) return s;
-      q0 = 1;
-    } else if ((s = enqueue_h(jev[33]))) {
-      return s;
-    }
-    for (int q = q0; q < nbig; q++) {
-      if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-      if ((s = sort_job(big[q], sS))) return s;
-    }
-    for (int q = q0; q < nbig; q++)
-      if ((s = acc_job(big[q], sA))) return s;
   }
+  for (int q = 0; q < pre_sorts; q++) {
+    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if ((s = sort_job(big[q], sS))) return s;
+  }
+  if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
+  if (nbig > 0) {
+    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + big[pre_sorts - 1]], 0));
+    if ((s = acc_job(big[0], sA))) return s;
+  }
+  const auto t_acc0 = std::chrono::steady_clock::now();
+  if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
+  for (int q = pre_sorts; q < nbig; q++) {
+    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if ((s = sort_job(big[q], sS))) return s;
+  }
+  for (int q = 1; q < nbig; q++)
+    if ((s = acc_job(big[q], sA))) return s;
+  if ((s = run_small())) return s;
   for (int q = 0; q < nbig; q++)
     if ((s = tail_job(big[q], tails[q]))) return s;
-  if ((s = run_small())) return s;
+  const auto t_enq = std::chrono::steady_clock::now();
   BH_TRY_HIP(hipStreamSynchronize(sS));
   BH_TRY_HIP(hipStreamSynchronize(sA));
   BH_TRY_HIP(hipStreamSynchronize(sH));
   BH_TRY_HIP(hipStreamSynchronize(sT));
   for (int q = 0; q < nbig; q++) BH_TRY_HIP(hipStreamSynchronize(tails[q]));
+  const auto t_gpu = std::chrono::steady_clock::now();
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0, g1_adds = 0, g2_adds = 0;
   int g1_launches = 0, g2_launches = 0;
@@ -648,6 +649,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
 
   const auto t1 = std::chrono::steady_clock::now();
+  static const bool host_timing = getenv("BH_HOST_TIMING") != nullptr;
+  if (host_timing) {
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, enqueue done %.3f, gpu done %.3f, combine %.3f\n",
+            ms(t0, t_acc0), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
+  }
   float h_ms = 0;
   hipEventElapsedTime(&h_ms, ctx->ev[0], ctx->ev[1]);
   ctx->last_timings[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
@@ -727,7 +736,9 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
   if (s) return s;
   const auto t0 = std::chrono::steady_clock::now();
   assemble(vk_of(params), r1, r2, r_in, s_in, proof_out);
-  ctx->last_timings[0] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double asm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ctx->last_timings[0] += asm_ms;
+  if (getenv("BH_HOST_TIMING")) fprintf(stderr, "assemble %.3f ms\n", asm_ms);
   return BH_OK;
 }
 
