@@ -122,6 +122,7 @@ struct bh_ctx {
   bh::DevBuf idx;         // density index map
   bh::DevBuf dtmp;        // density scan tmp
   bh::DevBuf dscan;       // scan scratch
+  bh::DevBuf dscan2;      // scan scratch of derived (compacted) sorts
   bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};

@@ -343,6 +343,64 @@ __global__ void __launch_bounds__(256) k_part_sort(const uint2* recs, const uint
   }
 }
 
+// ----------------------------------------------------------------- derived sorts
+// A multiexp over the same scalars and digit geometry as an already sorted one, but a
+// sparser density map (a_aux, b_aux against l: prover.rs:259-307 all take the aux assignment),
+// has the same bucket order: its sorted entries are the source's with every entry whose
+// scalar is absent dropped and the base index remapped -- a stable compaction.
+__device__ __forceinline__ bool derive_keep(uint32_t e, int pre, uint32_t W, uint32_t src_off, const int32_t* idx,
+                                            uint32_t* out_entry) {
+  const uint32_t v = e & 0x7fffffffu;
+  const uint32_t base = pre ? v / W : v;
+  const int32_t nb = idx[base - src_off];
+  if (nb < 0) return false;
+  *out_entry = ((pre ? (uint32_t)nb * W + (v - base * W) : (uint32_t)nb)) | (e & 0x80000000u);
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_derive_mark(const uint32_t* src_entries, const uint32_t* src_E, size_t Emax,
+                                                     int pre, uint32_t W, uint32_t src_off, const int32_t* idx,
+                                                     uint32_t* mark) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > Emax) return;
+  uint32_t ne;
+  mark[j] = (j < *src_E && derive_keep(src_entries[j], pre, W, src_off, idx, &ne)) ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(256) k_derive_write(const uint32_t* src_entries, const uint32_t* src_E, int pre,
+                                                      uint32_t W, uint32_t src_off, const int32_t* idx,
+                                                      const uint32_t* pos, uint32_t* dst_entries) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= *src_E) return;
+  uint32_t ne;
+  if (derive_keep(src_entries[j], pre, W, src_off, idx, &ne)) dst_entries[pos[j]] = ne;
+}
+
+__global__ void __launch_bounds__(256) k_derive_offsets(const uint32_t* src_offsets, size_t nbt, const uint32_t* pos,
+                                                        uint32_t* dst_offsets, uint32_t* dst_counts) {
+  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nbt) return;
+  const uint32_t o = pos[src_offsets[b]];
+  dst_offsets[b] = o;
+  if (b < nbt) dst_counts[b] = pos[src_offsets[b + 1]] - o;
+}
+
+size_t derive_scratch_words(size_t Emax) { return scan_scratch_words(Emax + 1) + 64; }
+
+hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offsets, size_t nbt, size_t Emax, int pre,
+                         uint32_t W, uint32_t src_off, const int32_t* idx, uint32_t* pos, uint32_t* scan_scratch,
+                         uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st) {
+  const uint32_t* src_E = src_offsets + nbt;
+  hipLaunchKernelGGL(k_derive_mark, dim3(blocks_for(Emax + 1, 256)), dim3(256), 0, st, src_entries, src_E, Emax, pre, W,
+                     src_off, idx, pos);
+  exclusive_scan(pos, pos, Emax + 1, scan_scratch, st);
+  hipLaunchKernelGGL(k_derive_write, dim3(blocks_for(Emax, 256)), dim3(256), 0, st, src_entries, src_E, pre, W, src_off,
+                     idx, pos, dst_entries);
+  hipLaunchKernelGGL(k_derive_offsets, dim3(blocks_for(nbt + 1, 256)), dim3(256), 0, st, src_offsets, nbt, pos,
+                     dst_offsets, dst_counts);
+  return hipGetLastError();
+}
+
 void sort_geometry(const MsmShape& sh, size_t n, int* lo_bits, uint32_t* P, uint32_t* ntiles) {
   const size_t nbt = (size_t)sh.Wb * sh.NB;
   int bits = 0;

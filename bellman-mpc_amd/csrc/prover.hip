@@ -481,6 +481,16 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     return jobs[i].sc == jobs[j].sc && jobs[i].idx == jobs[j].idx && los[i] == los[j] && his[i] == his[j] &&
            a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre;
   };
+  // ... and one over a sparser density map (a_aux, b_aux under l's dense one) compacts it
+  static const bool derive_on = [] {  // BH_SORT_DERIVE=0: full sorts only (A/B experiments)
+    const char* e = getenv("BH_SORT_DERIVE");
+    return !(e && e[0] == '0');
+  }();
+  auto derivable = [&](int i, int j) {
+    const MsmShape &a = shapes[i], &b = shapes[j];
+    return derive_on && jobs[i].sc == jobs[j].sc && !jobs[i].idx && jobs[j].idx && !jobs[i].is_h && los[i] == los[j] &&
+           his[i] == his[j] && a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre;
+  };
   int sorted_from[8];
   for (int j = 0; j < 8; j++) sorted_from[j] = -1;
   auto sort_job = [&](int j, hipStream_t st) -> bh_status {
@@ -491,7 +501,31 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     int src = -1;
     for (int i = 0; i < 8 && src < 0; i++)
       if (i != j && sorted_from[i] == i && same_digits(i, j)) src = i;
-    if (src >= 0) {
+    int dsrc = -1;  // a fully dense sort over the same scalars and digits to compact from
+    for (int i = 0; i < 8 && src < 0 && dsrc < 0; i++)
+      if (i != j && sorted_from[i] == i && derivable(i, j)) dsrc = i;
+    if (dsrc >= 0) {
+      const MsmShape& sh = shapes[j];
+      const size_t nbt = (size_t)sh.Wb * sh.NB, Emax = n * (size_t)sh.W;
+      const auto& S = jobs[dsrc];
+      const uint32_t* se = S.g2 ? ctx->pw2[S.out].entries : ctx->pw1[S.out].entries;
+      const uint32_t* so = S.g2 ? ctx->pw2[S.out].offsets : ctx->pw1[S.out].offsets;
+      uint32_t *de, *dc, *dof, *pos;
+      if (J.g2) {
+        BH_TRY_HIP(ctx->pw2[J.out].reserve_shape(n, sh));
+        de = ctx->pw2[J.out].entries; dc = ctx->pw2[J.out].counts; dof = ctx->pw2[J.out].offsets;
+        pos = reinterpret_cast<uint32_t*>(ctx->pw2[J.out].recs);
+      } else {
+        BH_TRY_HIP(ctx->pw1[J.out].reserve_shape(n, sh));
+        de = ctx->pw1[J.out].entries; dc = ctx->pw1[J.out].counts; dof = ctx->pw1[J.out].offsets;
+        pos = reinterpret_cast<uint32_t*>(ctx->pw1[J.out].recs);
+      }
+      BH_TRY_HIP(ctx->dscan2.alloc(derive_scratch_words(Emax) * 4));
+      BH_TRY_HIP(hipStreamWaitEvent(st, jev[16 + dsrc], 0));
+      BH_TRY_HIP(derive_sorted(se, so, nbt, Emax, sh.pre, (uint32_t)sh.W, (uint32_t)los[dsrc], ix, pos,
+                               ctx->dscan2.as<uint32_t>(), de, dc, dof, st));
+      sorted_from[j] = j;  // a sort of its own from here on (copies may take it)
+    } else if (src >= 0) {
       const MsmShape& sh = shapes[j];
       const size_t nbt = (size_t)sh.Wb * sh.NB;
       const uint32_t *e, *cn, *of;
@@ -596,25 +630,36 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // a whole-GPU accumulation only gets CUs as its workgroups retire, so the second one would
   // not be ready when the first accumulation ends), the first accumulation, H, the remaining
   // sorts (h's after H), every accumulation, the small multiexps, then the tails.
-  const int pre_sorts = std::min(nbig, h_pos == 1 ? 1 : 2);
-  if (h_pos < pre_sorts && h_mode == 2) h_mode = 1;  // h's own sort is among the first: H first
+  // Sort order = accumulation order (b_g2_aux sorted, b_g1_aux copied, l sorted, a_aux
+  // compacted from l, h): putting l first so that b_g2_aux could be compacted from it would
+  // lengthen the start-up (measured +2 ms at 2^22), so only later sorts are derived.
+  int sorder[8];
+  const int ns = nbig;
+  for (int q = 0; q < nbig; q++) sorder[q] = big[q];
+  // every sort up to those of the first two accumulations runs ahead of the first accumulation
+  int pre_sorts = 0;
+  for (int r = 0; r < ns; r++)
+    if (sorder[r] == big[0] || (nbig > 1 && h_pos != 1 && sorder[r] == big[1])) pre_sorts = r + 1;
+  bool h_in_pre = false;
+  for (int r = 0; r < pre_sorts; r++) h_in_pre = h_in_pre || jobs[sorder[r]].is_h;
+  if (h_in_pre && h_mode == 2) h_mode = 1;  // h's own sort is among the first: H first
   if (h_mode == 0 || h_mode == 1) {
     if ((s = enqueue_h(jev[33]))) return s;
   }
-  for (int q = 0; q < pre_sorts; q++) {
-    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    if ((s = sort_job(big[q], sS))) return s;
+  for (int r = 0; r < pre_sorts; r++) {
+    if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if ((s = sort_job(sorder[r], sS))) return s;
   }
   if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
   if (nbig > 0) {
-    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + big[pre_sorts - 1]], 0));
+    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + sorder[pre_sorts - 1]], 0));
     if ((s = acc_job(big[0], sA))) return s;
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
-  for (int q = pre_sorts; q < nbig; q++) {
-    if (q == h_pos) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    if ((s = sort_job(big[q], sS))) return s;
+  for (int r = pre_sorts; r < ns; r++) {
+    if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    if ((s = sort_job(sorder[r], sS))) return s;
   }
   for (int q = 1; q < nbig; q++)
     if ((s = acc_job(big[q], sA))) return s;
