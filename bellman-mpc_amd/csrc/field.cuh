@@ -338,22 +338,21 @@ constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
 
 struct Fp2Ops {
   using T = DFp2;
-  static constexpr uint32_t MB = 6;
+  static constexpr uint32_t MB = 2;
+  // Schoolbook over two interleaved reductions: c0 = a0 b0 + (128p - a1) b1, c1 = a0 b1 + a1 b0.
+  // One reduction fewer than Karatsuba's three muls, no pre-additions, and both halves
+  // come out < 2p; valid for inputs < 128p.
   static BH_DEV T mul(const T& a, const T& b) {
-    DFp t0 = fe_mul<FpCfg>(a.c0, b.c0);
-    DFp t1 = fe_mul<FpCfg>(a.c1, b.c1);
-    DFp t2 = fe_mul<FpCfg>(fe_add<FpCfg>(a.c0, a.c1), fe_add<FpCfg>(b.c0, b.c1));
     T r;
-    r.c0 = fe_sub<FpCfg, 2>(t0, t1);                       // < 4p
-    r.c1 = fe_sub<FpCfg, 4>(t2, fe_add<FpCfg>(t0, t1));     // < 6p
+    r.c0 = fe_mul2<FpCfg>(a.c0, b.c0, fe_neg<FpCfg, 128>(a.c1), b.c1);
+    r.c1 = fe_mul2<FpCfg>(a.c0, b.c1, a.c1, b.c0);
     return r;
   }
   static BH_DEV T sqr(const T& a) {
     T r;
-    // (a0 + a1)(a0 - a1), 2 a0 a1 ; valid for inputs < 128p
+    // (a0 + a1)(a0 - a1), (2 a0) a1 ; valid for inputs < 128p, both < 2p
     r.c0 = fe_mul<FpCfg>(fe_add<FpCfg>(a.c0, a.c1), fe_sub<FpCfg, 128>(a.c0, a.c1));
-    DFp t = fe_mul<FpCfg>(a.c0, a.c1);
-    r.c1 = fe_add<FpCfg>(t, t);                              // < 4p
+    r.c1 = fe_mul<FpCfg>(fe_add<FpCfg>(a.c0, a.c0), a.c1);
     return r;
   }
   static BH_DEV T add(const T& a, const T& b) {

@@ -19,7 +19,8 @@
 
 namespace bh {
 
-static constexpr int NTT_E = 1024;  // elements per workgroup
+static constexpr int NTT_LG_E = 10;
+static constexpr int NTT_E = 1 << NTT_LG_E;  // elements per workgroup
 static constexpr int NTT_T = 256;   // threads per workgroup
 
 struct PassArgs {
@@ -46,7 +47,8 @@ template <bool DIF>
 __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) {
   __shared__ uint32_t lds[9 * NTT_E];
   const int D = a.D;
-  const uint32_t G = NTT_E >> D;             // groups per workgroup
+  const int lgG = NTT_LG_E - D;
+  const uint32_t G = 1u << lgG;              // groups per workgroup (index math by shifts)
   const uint32_t total_groups = 1u << (a.L - D);
   const uint32_t g0 = blockIdx.x * G;
   const uint32_t stride = DIF ? (1u << (a.L - a.t - D)) : (1u << a.t);  // distance between consecutive lo's
@@ -55,12 +57,12 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
   // ---- load
   for (uint32_t e = threadIdx.x; e < (uint32_t)NTT_E; e += NTT_T) {
     uint32_t gl, k;
-    if (lo_fast) { gl = e % G; k = e / G; } else { k = e & (K - 1); gl = e >> D; }
+    if (lo_fast) { gl = e & (G - 1); k = e >> lgG; } else { k = e & (K - 1); gl = e >> D; }
     const uint32_t g = g0 + gl;
     if (g >= total_groups) continue;
     const uint32_t idx = DIF ? dif_index(a, g, k) : dit_index(a, g, k);
     DFr x = ld_packed(data, idx);
-    const uint32_t slot = k * G + gl;
+    const uint32_t slot = (k << lgG) + gl;
 #pragma unroll
     for (int l = 0; l < 9; l++) lds[l * NTT_E + slot] = x.v[l];
   }
@@ -69,12 +71,12 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
   for (int j = 0; j < D; j++) {
     const int u = a.t + j;  // global stage
     for (uint32_t b = threadIdx.x; b < (uint32_t)(NTT_E / 2); b += NTT_T) {
-      const uint32_t gl = b % G, r = b / G;
+      const uint32_t gl = b & (G - 1), r = b >> lgG;
       if (g0 + gl >= total_groups) continue;
       const int hb = DIF ? (D - 1 - j) : j;  // pair distance 2^hb in k
       const uint32_t k = ((r >> hb) << (hb + 1)) | (r & ((1u << hb) - 1));
       const uint32_t k2 = k + (1u << hb);
-      const uint32_t s0 = k * G + gl, s1 = k2 * G + gl;
+      const uint32_t s0 = (k << lgG) + gl, s1 = (k2 << lgG) + gl;
       DFr x, y;
 #pragma unroll
       for (int l = 0; l < 9; l++) { x.v[l] = lds[l * NTT_E + s0]; y.v[l] = lds[l * NTT_E + s1]; }
@@ -106,11 +108,11 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
   // ---- store (+ optional post-scale by natural index)
   for (uint32_t e = threadIdx.x; e < (uint32_t)NTT_E; e += NTT_T) {
     uint32_t gl, k;
-    if (lo_fast) { gl = e % G; k = e / G; } else { k = e & (K - 1); gl = e >> D; }
+    if (lo_fast) { gl = e & (G - 1); k = e >> lgG; } else { k = e & (K - 1); gl = e >> D; }
     const uint32_t g = g0 + gl;
     if (g >= total_groups) continue;
     const uint32_t idx = DIF ? dif_index(a, g, k) : dit_index(a, g, k);
-    const uint32_t slot = k * G + gl;
+    const uint32_t slot = (k << lgG) + gl;
     DFr x;
 #pragma unroll
     for (int l = 0; l < 9; l++) x.v[l] = lds[l * NTT_E + slot];

@@ -444,8 +444,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
     else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
   }
-  // ---- H (prover.rs:210-234), device resident.  It starts once the first sort is done
-  // (so it does not delay the first accumulation) and is only needed by h's sort.
+  // ---- H (prover.rs:210-234), device resident.  Where it is enqueued depends on h_mode
+  // (below); only h's sort waits for it.
   auto enqueue_h = [&](hipEvent_t after) -> bh_status {
     BH_TRY_HIP(hipStreamWaitEvent(sH, after, 0));
     hipEventRecord(ctx->ev[0], sH);

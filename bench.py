@@ -32,7 +32,7 @@ G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point
 G2_PAIR_BYTES = 224
 TRAFFIC_FILE = "r01_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
 G1_MADD_PEAK = 6.51            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X
-MADS_PER_G1_MADD = 8 * 391 + 2 * 300
+MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
 
 
@@ -219,7 +219,7 @@ def main():
             "algorithmic_bytes_per_launch": round(pairs * G1_PAIR_BYTES / launches) if launches else None,
             "note": "VALU-bound (XYZZ mixed additions on 29-bit limbs): see DESIGN.md section 4"}
     # integer-ALU roofline: G1 mixed additions/s against the microbenchmarked peak, and the
-    # v_mad_u64_u32 issue rate they imply (8 Fp-mul x 391 + 2 Fp-sqr x 300 per addition)
+    # v_mad_u64_u32 issue rate they imply (see MADS_PER_G1_MADD)
     g1_adds = sum(t[8] for t in timings)
     madd_rate = g1_adds / (acc_ms / 1e3) / 1e9 if acc_ms > 0 else None
     valu = {"kernel": "k_accumulate_pf<G1>", "unit": "G mixed-add/s",

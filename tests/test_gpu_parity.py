@@ -444,3 +444,42 @@ def test_distributed_h_partials_equal_single_proof(ctx, logc, nshards):
     single = bh.prove_witness(ctx, params, w, 27134, 17146)
     parts = bh.prove_witness_partials_local(ctx, params, w, nshards)
     assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146) == single
+
+
+def test_polynomial_arith_fft_product_equals_naive(ctx):
+    """domain.rs:378-420 (polynomial_arith): fft(a) * fft(b), then ifft, equals the naive
+    product; lengths sampled from the reference's 0..70 x 0..70 sweep, incl. empty."""
+    bh = _bh()
+    rng = random.Random(378)
+    lens = [0, 1, 2, 3, 5, 8, 13, 31, 32, 33, 64, 69]
+    for la in lens:
+        for lb in lens:
+            a = [rng.randrange(R) for _ in range(la)]
+            b = [rng.randrange(R) for _ in range(lb)]
+            naive = [0] * (la + lb)
+            for i, x in enumerate(a):
+                for j, y in enumerate(b):
+                    naive[i + j] = (naive[i + j] + x * y) % R
+            da = bh.EvaluationDomain(ctx, a + [0] * lb)
+            db = bh.EvaluationDomain(ctx, b + [0] * la)
+            da.fft()
+            db.fft()
+            da.mul_assign(db)
+            da.ifft()
+            got = list(da.into_coeffs())
+            assert got[: la + lb] == naive, (la, lb)
+            assert all(v == 0 for v in got[la + lb:]), (la, lb)
+
+
+@pytest.mark.parametrize("logm", range(0, 10))
+def test_fft_composition(ctx, logm):
+    """domain.rs:429-463 (fft_composition): ifft/fft, fft/ifft, icoset/coset and coset/icoset
+    are identities on random full-width Fr vectors of length 2^0 .. 2^9."""
+    bh = _bh()
+    rng = random.Random(429 + logm)
+    v = [rng.randrange(R) for _ in range(1 << logm)]
+    d = bh.EvaluationDomain(ctx, v)
+    for first, second in (("ifft", "fft"), ("fft", "ifft"), ("icoset_fft", "coset_fft"), ("coset_fft", "icoset_fft")):
+        getattr(d, first)()
+        getattr(d, second)()
+        assert list(d.into_coeffs()) == v, (first, second)
