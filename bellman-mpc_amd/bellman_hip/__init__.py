@@ -117,6 +117,14 @@ def _load():
         "bh_chain_witness_preimage": (I, [P, S, U64, U64, P]),
         "bh_prove_witness_partial_comm": (I, [P, P, P, P, P]),
         "bh_prove_witness_partials_local": (I, [P, P, P, S, P]),
+        "bh_comm_allgather": (I, [P, P, S, P]),
+        "bh_params_prepare_shard": (I, [P, P, P, S, S, I]),
+        "bh_last_stats": (I, [P, P, S]),
+        "bh_prove_witness_partials_ranks": (I, [P, P, P, S, P]),
+        "bh_chain_sizes": (I, [S, P]),
+        "bh_chain_assignment": (I, [S, U64, U64, P, P, P, P, P, P, P, P]),
+        "bh_comm_allreduce_max": (I, [P, P]),
+        "bh_comm_info": (I, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -138,6 +146,8 @@ EXPORTED_SYMBOLS = [
     "bh_vk_write", "bh_proof_from_partials", "bh_comm_unique_id", "bh_comm_init", "bh_comm_allgather_partials",
     "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count", "bh_ctx_set_tables", "bh_params_prepare",
     "bh_chain_witness_preimage", "bh_prove_witness_partial_comm", "bh_prove_witness_partials_local",
+    "bh_comm_allgather", "bh_comm_allreduce_max", "bh_comm_info", "bh_params_prepare_shard", "bh_last_stats",
+    "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment",
 ]
 PARTIAL_BYTES = 960
 
@@ -223,6 +233,12 @@ class Context:
         """bh_last_timings: see include/bellman_hip.h for the 10 fields."""
         out = (ctypes.c_double * 10)()
         _check(_lib.bh_last_timings(self.h, out))
+        return list(out)
+
+    def last_stats(self):
+        """bh_last_stats: the 10 timing fields, then tables used / large multiexps / table bytes."""
+        out = (ctypes.c_double * 13)()
+        _check(_lib.bh_last_stats(self.h, out, 13))
         return list(out)
 
     def close(self):
@@ -390,6 +406,11 @@ class Parameters:
     def prepare(self, witness, nshards=1):
         """Build the prover window tables now rather than inside the first proof."""
         _check(_lib.bh_params_prepare(self.ctx.h, self.h, witness.h, nshards), "bh_params_prepare")
+
+    def prepare_shard(self, witness, shard, nshards, distributed_h=True):
+        """Build only the table slices shard `shard` of `nshards` uses (a rank's 1/N share)."""
+        _check(_lib.bh_params_prepare_shard(self.ctx.h, self.h, witness.h, shard, nshards, int(bool(distributed_h))),
+               "bh_params_prepare_shard")
 
     def vk_bytes(self):
         """VerifyingKey::write (groth16/mod.rs:146-159)."""
@@ -568,6 +589,36 @@ def prove_witness(ctx, params, witness, r, s):
     return out.tobytes()
 
 
+def chain_assignment(rounds, seed=7, preimage_seed=None):
+    """The MiMC chain's ProvingAssignment on the host (bh_chain_assignment) in the layouts of
+    bh_prove: a/b/c/inputs/aux as (n,4) uint64 Montgomery, densities as uint64 bit words."""
+    sz = (ctypes.c_size_t * 3)()
+    _check(_lib.bh_chain_sizes(rounds, sz), "bh_chain_sizes")
+    nc, ni, na = sz
+    out = {k: np.zeros((n, 4), dtype=np.uint64) for k, n in (("a", nc), ("b", nc), ("c", nc), ("inputs", ni),
+                                                              ("aux", na))}
+    out["a_aux_density"] = np.zeros((na + 63) // 64, dtype=np.uint64)
+    out["b_input_density"] = np.zeros((ni + 63) // 64, dtype=np.uint64)
+    out["b_aux_density"] = np.zeros((na + 63) // 64, dtype=np.uint64)
+    ps = seed + 1 if preimage_seed is None else preimage_seed
+    _check(_lib.bh_chain_assignment(rounds, seed, ps, *[_ptr(out[k]) for k in (
+        "a", "b", "c", "inputs", "aux", "a_aux_density", "b_input_density", "b_aux_density")]), "bh_chain_assignment")
+    return out
+
+
+def prove(ctx, params, asg, r, s):
+    """bh_prove: create_proof after synthesis straight from host buffers (the drop-in entry
+    point of INTEGRATION.md section 1).  asg: dict as returned by chain_assignment."""
+    out = np.zeros(192, dtype=np.uint8)
+    rr, ss = fr_to_canonical_limbs([r])[0], fr_to_canonical_limbs([s])[0]
+    A = [np.ascontiguousarray(asg[k], dtype=np.uint64) for k in ("a", "b", "c", "inputs", "aux")]
+    D = [np.ascontiguousarray(asg[k], dtype=np.uint64) for k in ("a_aux_density", "b_input_density", "b_aux_density")]
+    _check(_lib.bh_prove(ctx.h, params.h, _ptr(A[0]), _ptr(A[1]), _ptr(A[2]), A[0].shape[0], _ptr(A[3]),
+                         A[3].shape[0], _ptr(A[4]), A[4].shape[0], _ptr(D[0]), _ptr(D[1]), _ptr(D[2]), _ptr(rr),
+                         _ptr(ss), _ptr(out)), "bh_prove")
+    return out.tobytes()
+
+
 def create_proof(ctx, circuit, params, r, s):
     """prover.rs:175-350: synthesize on the host, prove on the device."""
     p = synthesize(circuit)
@@ -599,6 +650,17 @@ def prove_witness_partials_local(ctx, params, witness, nshards):
     copies): the multi-GPU algorithm end to end without a second GPU."""
     out = np.zeros(nshards * PARTIAL_BYTES, dtype=np.uint8)
     _check(_lib.bh_prove_witness_partials_local(ctx.h, params.h, witness.h, nshards, _ptr(out)), "partials_local")
+    return out.tobytes()
+
+
+def prove_witness_partials_ranks(ctxs, params_list, witness):
+    """N ranks of one device with their own contexts and Parameters (bh_prove_witness_partials_ranks)."""
+    n = len(ctxs)
+    assert len(params_list) == n
+    ca = (ctypes.c_void_p * n)(*[c.h.value for c in ctxs])
+    pa = (ctypes.c_void_p * n)(*[p.h.value for p in params_list])
+    out = np.zeros(n * PARTIAL_BYTES, dtype=np.uint8)
+    _check(_lib.bh_prove_witness_partials_ranks(ca, pa, witness.h, n, _ptr(out)), "partials_ranks")
     return out.tobytes()
 
 
@@ -645,6 +707,25 @@ class Comm:
         out = np.zeros(self.nranks * PARTIAL_BYTES, dtype=np.uint8)
         _check(_lib.bh_comm_allgather_partials(self.h, _ptr(src), _ptr(out)), "ncclAllGather")
         return out.tobytes()
+
+    def allgather_bytes(self, rec):
+        """Every rank's equal-length record, rank order (bh_comm_allgather)."""
+        src = np.frombuffer(bytes(rec), dtype=np.uint8)
+        out = np.zeros(self.nranks * src.size, dtype=np.uint8)
+        _check(_lib.bh_comm_allgather(self.h, _ptr(src), src.size, _ptr(out)), "ncclAllGather")
+        return [out[k * src.size:(k + 1) * src.size].tobytes() for k in range(self.nranks)]
+
+    def allreduce_max(self, x):
+        """Max of x over the ranks; also a barrier (bh_comm_allreduce_max)."""
+        v = ctypes.c_double(float(x))
+        _check(_lib.bh_comm_allreduce_max(self.h, ctypes.byref(v)), "ncclAllReduce")
+        return v.value
+
+    def info(self):
+        """(rank count, this rank, HIP device) as RCCL reports them."""
+        out = (ctypes.c_int * 3)()
+        _check(_lib.bh_comm_info(self.h, out), "bh_comm_info")
+        return tuple(out)
 
     def close(self):
         if self.h:

@@ -401,6 +401,13 @@ static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const F
   return BH_OK;
 }
 
+void ctx_sync_all(bh_ctx* ctx) {
+  for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
+    if (st) (void)hipStreamSynchronize(st);
+  for (hipStream_t st : ctx->tstream)
+    if (st) (void)hipStreamSynchronize(st);
+}
+
 bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
   auto it = ctx->domains.find(L);
   if (it != ctx->domains.end()) { *out = it->second.get(); return BH_OK; }
@@ -599,11 +606,10 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
 
 bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (!ctx) return BH_OK;
+  for (bh_ctx* v : ctx->vranks) bh_ctx_destroy(v);
+  ctx->vranks.clear();
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
-  (void)hipStreamSynchronize(ctx->stream2);
-  (void)hipStreamSynchronize(ctx->stream3);
-  (void)hipStreamSynchronize(ctx->stream4);
+  ctx_sync_all(ctx);  // nothing may still read the workspaces released below
   ctx->g1ws.release();
   ctx->g2ws.release();
   for (auto& w : ctx->pw1) w.release();
@@ -618,10 +624,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream4);
-  for (auto& t : ctx->tstream) {
-    (void)hipStreamSynchronize(t);
-    (void)hipStreamDestroy(t);
-  }
+  for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
   delete ctx->dist;
   delete ctx;
   return BH_OK;

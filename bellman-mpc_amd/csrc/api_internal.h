@@ -5,6 +5,8 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
+#include <tuple>
 #include <vector>
 
 #include "../../include/bellman_hip.h"
@@ -70,19 +72,37 @@ struct bh_srs {
   size_t n = 0;
   bh::DevBuf pts;                    // packed affine, device Montgomery
   std::vector<size_t> identity_idx;  // indices of points at infinity (rejected by next())
-  // prover window table (built lazily, see prepare_tables in prover.hip):
-  // win[i*win_W + w] = 2^(win_c*w) * P_i, packed affine
+  // prover window table (built lazily, see prepare_tables in prover.hip) over the bases
+  // [win_lo, win_hi) -- a shard's slice or the whole vector:
+  // win[(i - win_lo)*win_W + w] = 2^(win_c*w) * P_i, packed affine, one record per win_rec words
   bh::DevBuf win;
   int win_c = 0, win_W = 0, win_rec = 0;  // win_rec: u32 words per record (128-B aligned)
+  size_t win_lo = 0, win_hi = 0;
+  // the table addressed by GLOBAL base index (entries encode i*W + w): the allocation shifted
+  // back by win_lo records (only indices in [win_lo, win_hi) are ever formed)
+  const uint32_t* win_global() const {
+    return reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(win.p) -
+                                             (uintptr_t)win_lo * (uintptr_t)win_W * (uintptr_t)win_rec * 4u);
+  }
+  bool win_covers(int c, size_t lo, size_t hi) const { return win_c == c && win_c && win_lo <= lo && hi <= win_hi; }
+  // the last table request that could not be met (HBM short): not retried every proof
+  int skip_c = 0;
+  size_t skip_lo = 0, skip_hi = 0;
 };
 
 struct bh_params {
   bh_ctx* ctx = nullptr;
+  // window tables and h shares: built under an exclusive lock, read by proofs under a shared
+  // one (several contexts of one device may prove with one Parameters)
+  std::shared_mutex mu;
   // VerifyingKey (host form)
   bh::AffinePt<bh::Fp> alpha_g1, beta_g1, delta_g1;
   bh::AffinePt<bh::Fp2> beta_g2, gamma_g2, delta_g2;
   std::vector<bh::AffinePt<bh::Fp>> ic;
   bh_srs h, l, a, b_g1, b_g2;
+  // h bases of one rank's distributed-H share (dist_h.h: h[M*t + q], q in the rank's chunk),
+  // gathered into share order so that a shard-sized window table covers them; key (N, rank, L)
+  std::map<std::tuple<int, int, int>, std::unique_ptr<bh_srs>> h_shares;
 };
 
 struct bh_witness {
@@ -95,6 +115,8 @@ struct bh_witness {
   size_t a_aux_words = 0, b_in_words = 0, b_aux_words = 0;
   std::vector<uint64_t> a_aux_density, b_input_density, b_aux_density;  // host copies (EOF checks)
   size_t a_aux_total = 0, b_in_total = 0, b_aux_total = 0;
+  // set bits before word k of each density map (k = 0..words): base index of a scalar shard
+  std::vector<size_t> a_aux_prefix, b_aux_prefix;
 };
 
 struct bh_ctx {
@@ -126,15 +148,18 @@ struct bh_ctx {
   bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
-  double last_timings[10] = {};
+  double last_timings[16] = {};  // bh_last_timings [0,10) + bh_last_stats extras
   uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp,
                                     // [16,32) its continuation span (max_span)
   bh::DevBuf dspan;                 // device words for max_span
+  std::vector<bh_ctx*> vranks;      // bh_prove_witness_partials_local: the virtual ranks' contexts
   std::mutex mu;
 };
 
 namespace bh {
 bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out);
+// wait for every stream of the context (error paths, teardown)
+void ctx_sync_all(bh_ctx* ctx);
 // host <-> device Fr helpers
 void fr_to_dev_limbs(const Fr& x, uint32_t out[9]);
 void fr_to_dev_packed(const Fr& x, uint32_t out[8]);
@@ -156,11 +181,17 @@ bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n,
 bh_status multiexp_check(const bh_srs* bases, size_t base_offset, const uint64_t* density_words, size_t n,
                          const uint64_t* exps_canonical, bool need_exps);
 bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_affine_g1_or_g2, size_t n, bh_srs* out);
-// RCCL all-to-all of C-element packed-Fr chunks for the distributed H pipeline: for each of
-// nvec vectors of M = N*C elements, chunk p of send goes to rank p, which stores it as chunk
-// `this rank` of recv (comm.cpp)
-bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
-                        hipStream_t st);
+// The all-to-all step of the distributed H pipeline: for each of nvec vectors of M = N*C
+// packed-Fr elements, chunk p of send goes to rank p, which stores it as chunk `this rank` of
+// recv; stream-ordered on st.  Over RCCL (comm.cpp) or, to run the identical prover code with N
+// virtual ranks on one device, by device copies between threads (prover.hip).
+struct Exchanger {
+  virtual ~Exchanger() {}
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual bh_status exchange(const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec, hipStream_t st) = 0;
+};
+std::unique_ptr<Exchanger> rccl_exchanger(bh_comm* c);
 // smallest rank count that uses the distributed H pipeline (BH_DIST_H_MIN, default 4)
 size_t dist_h_min_ranks();
 int comm_rank(const bh_comm* c);

@@ -272,6 +272,41 @@ bh_status bh_chain_witness_preimage(bh_ctx* ctx, size_t rounds, uint64_t seed, u
                            cs.b_aux_density.data(), out);
 }
 
+bh_status bh_chain_sizes(size_t rounds, size_t out[3]) {
+  if (!out || rounds == 0) return BH_ERR_INVALID_ARGUMENT;
+  out[0] = 2 * rounds + 2;  // constraints: 2 per round + the 2 input constraints (prover.rs:198-204)
+  out[1] = 2;               // inputs: one, image
+  out[2] = 2 * rounds + 1;  // aux: xl, xr and one per round
+  return BH_OK;
+}
+
+bh_status bh_chain_assignment(size_t rounds, uint64_t seed, uint64_t preimage_seed, uint64_t* a, uint64_t* b,
+                              uint64_t* c, uint64_t* inputs, uint64_t* aux, uint64_t* a_aux_density,
+                              uint64_t* b_input_density, uint64_t* b_aux_density) {
+  size_t sz[3];
+  bh_status st = bh_chain_sizes(rounds, sz);
+  if (st) return st;
+  if (!a || !b || !c || !inputs || !aux || !a_aux_density || !b_input_density || !b_aux_density)
+    return BH_ERR_INVALID_ARGUMENT;
+  const std::vector<Fr> consts = fr_stream(seed, rounds);
+  const std::vector<Fr> pre = fr_stream(preimage_seed, 2);
+  ProvingAssignmentN cs;
+  cs.a.reserve(sz[0]); cs.b.reserve(sz[0]); cs.c.reserve(sz[0]);
+  cs.aux.reserve(sz[2]);
+  synthesize_chain(cs, consts, pre[0], pre[1]);
+  finish_inputs(cs, cs.inputs.size());
+  if (cs.a.size() != sz[0] || cs.inputs.size() != sz[1] || cs.aux.size() != sz[2]) return BH_ERR_INVALID_ARGUMENT;
+  memcpy(a, cs.a.data(), sz[0] * 32);
+  memcpy(b, cs.b.data(), sz[0] * 32);
+  memcpy(c, cs.c.data(), sz[0] * 32);
+  memcpy(inputs, cs.inputs.data(), sz[1] * 32);
+  memcpy(aux, cs.aux.data(), sz[2] * 32);
+  memcpy(a_aux_density, cs.a_aux_density.data(), (sz[2] + 63) / 64 * 8);
+  memcpy(b_input_density, cs.b_input_density.data(), (sz[1] + 63) / 64 * 8);
+  memcpy(b_aux_density, cs.b_aux_density.data(), (sz[2] + 63) / 64 * 8);
+  return BH_OK;
+}
+
 bh_status bh_chain_params(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t alpha_u, uint64_t beta_u,
                           uint64_t gamma_u, uint64_t delta_u, uint64_t tau_u, bh_params** out) {
   if (!ctx || !out || rounds == 0) return BH_ERR_INVALID_ARGUMENT;

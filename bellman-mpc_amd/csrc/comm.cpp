@@ -6,6 +6,7 @@
 // replacement for its single-process rayon fan-out (prover.rs:233-307).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -17,6 +18,7 @@ struct bh_comm {
   int nranks = 0, rank = 0;
   uint8_t* d_send = nullptr;
   uint8_t* d_recv = nullptr;
+  double* d_val = nullptr;  // bh_comm_allreduce_max
 };
 
 extern "C" {
@@ -39,9 +41,16 @@ bh_status bh_comm_init(bh_ctx* ctx, const uint8_t id[128], int nranks, int rank,
   c->rank = rank;
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof uid);
-  if (ncclCommInitRank(&c->comm, nranks, uid, rank) != ncclSuccess) { delete c; return BH_ERR_HIP; }
+  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    fprintf(stderr, "bh_comm_init(rank %d of %d, device %d): ncclCommInitRank: %s\n", rank, nranks, ctx->device,
+            ncclGetErrorString(r));
+    delete c;
+    return BH_ERR_HIP;
+  }
   if (hipMalloc(&c->d_send, BH_PARTIAL_BYTES) != hipSuccess ||
-      hipMalloc(&c->d_recv, (size_t)BH_PARTIAL_BYTES * nranks) != hipSuccess) {
+      hipMalloc(&c->d_recv, (size_t)BH_PARTIAL_BYTES * nranks) != hipSuccess ||
+      hipMalloc(&c->d_val, sizeof(double)) != hipSuccess) {
     ncclCommDestroy(c->comm);
     delete c;
     return BH_ERR_OUT_OF_MEMORY;
@@ -62,6 +71,46 @@ bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t
   return BH_OK;
 }
 
+// every rank's nbytes record, rank order (small host records: rank metadata, timings)
+bh_status bh_comm_allgather(bh_comm* c, const uint8_t* in, size_t nbytes, uint8_t* all_out) {
+  if (!c || !in || !all_out || nbytes == 0) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(c->ctx->mu);
+  BH_TRY_HIP(hipSetDevice(c->ctx->device));
+  hipStream_t st = c->ctx->stream;
+  bh::DevBuf d;
+  BH_TRY_HIP(d.alloc(nbytes * (size_t)(c->nranks + 1)));
+  uint8_t* ds = d.as<uint8_t>();
+  uint8_t* dr = ds + nbytes;
+  BH_TRY_HIP(hipMemcpyAsync(ds, in, nbytes, hipMemcpyHostToDevice, st));
+  if (ncclAllGather(ds, dr, nbytes, ncclUint8, c->comm, st) != ncclSuccess) return BH_ERR_HIP;
+  BH_TRY_HIP(hipMemcpyAsync(all_out, dr, nbytes * (size_t)c->nranks, hipMemcpyDeviceToHost, st));
+  BH_TRY_HIP(hipStreamSynchronize(st));
+  return BH_OK;
+}
+
+// max over ranks of *inout, every rank receiving it; completes only when every rank has
+// reached it, so it doubles as the barrier of a timed region
+bh_status bh_comm_allreduce_max(bh_comm* c, double* inout) {
+  if (!c || !inout) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(c->ctx->mu);
+  BH_TRY_HIP(hipSetDevice(c->ctx->device));
+  hipStream_t st = c->ctx->stream;
+  BH_TRY_HIP(hipMemcpyAsync(c->d_val, inout, sizeof(double), hipMemcpyHostToDevice, st));
+  if (ncclAllReduce(c->d_val, c->d_val, 1, ncclFloat64, ncclMax, c->comm, st) != ncclSuccess) return BH_ERR_HIP;
+  BH_TRY_HIP(hipMemcpyAsync(inout, c->d_val, sizeof(double), hipMemcpyDeviceToHost, st));
+  BH_TRY_HIP(hipStreamSynchronize(st));
+  return BH_OK;
+}
+
+// what RCCL itself reports for this communicator: out = {rank count, this rank, HIP device}
+bh_status bh_comm_info(const bh_comm* c, int out[3]) {
+  if (!c || !out) return BH_ERR_INVALID_ARGUMENT;
+  if (ncclCommCount(c->comm, &out[0]) != ncclSuccess || ncclCommUserRank(c->comm, &out[1]) != ncclSuccess ||
+      ncclCommCuDevice(c->comm, &out[2]) != ncclSuccess)
+    return BH_ERR_HIP;
+  return BH_OK;
+}
+
 }  // extern "C"
 
 namespace bh {
@@ -75,7 +124,7 @@ size_t dist_h_min_ranks() {
   return v;
 }
 
-bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
+static bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
                         hipStream_t st) {
   const size_t bytes = C * 32;
   for (int v = 0; v < nvec; v++) {  // own chunk: a device copy
@@ -101,6 +150,20 @@ bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t
 int comm_rank(const bh_comm* c) { return c->rank; }
 int comm_size(const bh_comm* c) { return c->nranks; }
 
+namespace {
+struct RcclExchanger : Exchanger {
+  bh_comm* c;
+  explicit RcclExchanger(bh_comm* cc) : c(cc) {}
+  int rank() const override { return c->rank; }
+  int size() const override { return c->nranks; }
+  bh_status exchange(const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec, hipStream_t st) override {
+    return comm_exchange(c, send, recv, C, M, nvec, st);
+  }
+};
+}  // namespace
+
+std::unique_ptr<Exchanger> rccl_exchanger(bh_comm* c) { return std::unique_ptr<Exchanger>(new RcclExchanger(c)); }
+
 }  // namespace bh
 
 extern "C" {
@@ -111,6 +174,7 @@ bh_status bh_comm_destroy(bh_comm* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->d_send) (void)hipFree(c->d_send);
   if (c->d_recv) (void)hipFree(c->d_recv);
+  if (c->d_val) (void)hipFree(c->d_val);
   delete c;
   return BH_OK;
 }

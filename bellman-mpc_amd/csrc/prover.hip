@@ -4,7 +4,9 @@
 #include <string.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
+#include <thread>
 
 #include "api_internal.h"
 #include "crs.h"
@@ -197,6 +199,13 @@ bh_status bh_witness_upload(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, c
   w->b_input_density.assign(b_input_density ? b_input_density : nullptr,
                             b_input_density ? b_input_density + w->b_in_words : nullptr);
   w->b_aux_density.assign(b_aux_density ? b_aux_density : nullptr, b_aux_density ? b_aux_density + w->b_aux_words : nullptr);
+  auto prefix = [](const std::vector<uint64_t>& d, size_t words) {
+    std::vector<size_t> pc(words + 1, 0);
+    for (size_t k = 0; k < words; k++) pc[k + 1] = pc[k] + (size_t)__builtin_popcountll(d[k]);
+    return pc;
+  };
+  w->a_aux_prefix = prefix(w->a_aux_density, w->a_aux_words);
+  w->b_aux_prefix = prefix(w->b_aux_density, w->b_aux_words);
   w->a_aux_total = popcount_words(w->a_aux_density, na);
   w->b_in_total = popcount_words(w->b_input_density, ni);
   w->b_aux_total = popcount_words(w->b_aux_density, na);
@@ -251,65 +260,247 @@ int table_c_for(size_t used_per_shard) {
   return used_per_shard >= TABLE_MIN_USED ? msm_table_c(used_per_shard) : 0;
 }
 
-bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c) {
-  if (c == 0 || srs->win_c == c) return BH_OK;
-  if (!srs->identity_idx.empty() || srs->n == 0) return BH_OK;  // identities: plain windows only
+// Window table of c-bit windows over the bases [lo, hi) of srs (a shard's slice, or the whole
+// vector): kept if the resident table already covers them at this c, else rebuilt for exactly
+// [lo, hi).  Skipped (plain windows, same results) when HBM is short -- reported once.
+bool table_wanted(const bh_srs* srs, int c, size_t lo, size_t hi) {
+  if (c == 0 || hi <= lo || srs->win_covers(c, lo, hi)) return false;
+  if (srs->skip_c == c && srs->skip_lo == lo && srs->skip_hi == hi) return false;  // HBM short last time
+  if (!srs->identity_idx.empty() || srs->n == 0 || hi > srs->n) return false;
+  return (unsigned __int128)hi * ((256 + c - 1) / c) < ((size_t)1 << 31);
+}
+
+bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
+  if (c == 0 || hi <= lo || srs->win_covers(c, lo, hi)) return BH_OK;
+  if (!srs->identity_idx.empty() || srs->n == 0 || hi > srs->n) return BH_OK;  // identities: plain windows only
   const int W = (256 + c - 1) / c;
-  if ((unsigned __int128)srs->n * W >= ((size_t)1 << 31)) return BH_OK;  // entry encoding limit
+  if ((unsigned __int128)hi * W >= ((size_t)1 << 31)) return BH_OK;  // entry encoding limit (global index)
   const bool g2 = srs->group == BH_G2;
   const uint32_t rec = g2 ? 64 : 32;  // 96 / 192-byte points padded to whole 128-byte lines
-  const size_t bytes = srs->n * W * rec * 4;
-  const size_t chunk = std::min<size_t>(srs->n, (size_t)1 << 19);
+  const size_t n = hi - lo;
+  const size_t bytes = n * W * rec * 4;
+  const size_t chunk = std::min<size_t>(n, (size_t)1 << 19);
   const size_t scratch = g2 ? window_table_scratch_bytes<G2Ops>(chunk, W) : window_table_scratch_bytes<G1Ops>(chunk, W);
   srs->win.release();
   srs->win_c = 0;
+  srs->win_lo = srs->win_hi = 0;
   size_t free_b = 0, total_b = 0;
   BH_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (bytes + scratch + ((size_t)4 << 30) > free_b) return BH_OK;  // keep 4 GB headroom
+  if (bytes + scratch + ((size_t)4 << 30) > free_b) {  // keep 4 GB headroom
+    if (srs->skip_c != c || srs->skip_lo != lo || srs->skip_hi != hi)
+      fprintf(stderr, "bellman_hip: window table skipped (%.2f GB needed, %.2f GB free): plain windows\n",
+              (bytes + scratch) / 1e9, free_b / 1e9);
+    srs->skip_c = c; srs->skip_lo = lo; srs->skip_hi = hi;
+    return BH_OK;
+  }
   BH_TRY_HIP(srs->win.alloc(bytes));
   DevBuf tmp;
   BH_TRY_HIP(tmp.alloc(scratch));
-  const uint32_t* pts = srs->pts.as<uint32_t>();
-  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
-  else BH_TRY_HIP(window_table<G1Ops>(pts, srs->n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
+  const uint32_t* pts = srs->pts.as<uint32_t>() + lo * (g2 ? 48 : 24);
+  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
+  else BH_TRY_HIP(window_table<G1Ops>(pts, n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   srs->win_c = c;
   srs->win_W = W;
   srs->win_rec = (int)rec;
+  srs->win_lo = lo;
+  srs->win_hi = hi;
   return BH_OK;
 }
 
-// the tables a proof of `w` on shard/nshards uses: h, l, a (aux part), b_g1, b_g2
-bh_status prepare_tables(bh_ctx* ctx, bh_params* params, size_t m, size_t na, size_t a_aux_used, size_t b_aux_used,
-                         size_t nshards) {
-  if (!ctx->tables || ctx->window_override) return BH_OK;
-  // BH_TABLE_C_FULL=1: window size chosen for the whole query, not the shard (A/B)
-  static const bool full_c = [] {
-    const char* e = getenv("BH_TABLE_C_FULL");
-    return e && e[0] == '1';
-  }();
-  const size_t N = full_c ? 1 : std::max<size_t>(nshards, 1);
-  bh_status s;
-  if ((s = ensure_table(ctx, &params->h, table_c_for((m - 1) / N)))) return s;
-  if ((s = ensure_table(ctx, &params->l, table_c_for(na / N)))) return s;
-  if ((s = ensure_table(ctx, &params->a, table_c_for(a_aux_used / N)))) return s;
-  if ((s = ensure_table(ctx, &params->b_g1, table_c_for(b_aux_used / N)))) return s;
-  return ensure_table(ctx, &params->b_g2, table_c_for(b_aux_used / N));
+// One multiexp of create_proof (prover.rs:233-307) as planned for a shard.
+struct Job {
+  bool g2 = false;
+  const bh_srs* srs = nullptr;  // bases: a Parameters vector, or a gathered h share
+  const uint32_t* sc = nullptr; // device scalars (canonical, packed)
+  size_t n = 0;                 // full query length (sharded below)
+  const int32_t* idx = nullptr; // device density map (global base index, -1 = absent) or null
+  size_t used = 0;              // density-set scalars (roofline accounting)
+  int out = 0;                  // result slot: G1 0..5 / G2 0..1
+  bool is_h = false;            // h: needs the H pipeline
+  bool presharded = false;      // n/idx are this shard's already (distributed H)
+  // host view for base ranges: dense (prefix == null) scalar i uses base boff + i; with a
+  // density map the set bits before i count the bases consumed
+  const std::vector<uint64_t>* hdens = nullptr;
+  const std::vector<size_t>* prefix = nullptr;
+  size_t boff = 0;
+  // filled by plan_shard
+  size_t lo = 0, hi = 0;    // this shard's scalars
+  size_t blo = 0, bhi = 0;  // the bases they consume
+  int table_c = 0;          // window size of this job's table (0: plain windows)
+};
+
+inline size_t dens_before(const Job& J, size_t i) {
+  if (!J.prefix) return i;
+  const size_t k = i / 64, r = i % 64;
+  size_t c = (*J.prefix)[k];
+  if (r) c += (size_t)__builtin_popcountll((*J.hdens)[k] & ((1ull << r) - 1ull));
+  return c;
 }
 
-// Where this shard's h scalars come from when they are not the replicated H pipeline's
-// range [shard*(m-1)/N, ...): a precomputed share (hbuf/hidx of a finished DistH, used by
-// the one-device emulation), or the distributed pipeline run here over RCCL.
-struct HSource {
-  const DistH* pre = nullptr;  // finished share: hbuf (canonical) + hidx, M entries
-  bh_comm* comm = nullptr;     // run DistH over this communicator (rank/nranks = shard/nshards)
+// The shape of the distributed-H share of rank `rank` of N at m = 2^L (dist_h.h): position
+// p = t*C + u holds h[M*t + rank*C + u]; the last rank's last position is the truncated
+// coefficient m-1 (prover.rs:227), so its share has M-1 scalars.
+struct ShareGeom {
+  int N = 0, rank = 0, L = 0;
+  size_t M = 0, C = 0;
+  size_t used() const { return rank == N - 1 ? M - 1 : M; }
 };
+
+// h bases of a share, gathered into share order (built once per Parameters, N, rank, L)
+bh_status ensure_h_share(bh_ctx* ctx, bh_params* params, const ShareGeom& g, bh_srs** out) {
+  auto key = std::make_tuple(g.N, g.rank, g.L);
+  auto it = params->h_shares.find(key);
+  if (it != params->h_shares.end()) { *out = it->second.get(); return BH_OK; }
+  std::unique_ptr<bh_srs> sh(new bh_srs());
+  sh->ctx = ctx;
+  sh->group = BH_G1;
+  sh->n = g.used();
+  BH_TRY_HIP(sh->pts.alloc(std::max<size_t>(sh->n, 1) * 96));
+  const uint8_t* src = params->h.pts.as<uint8_t>();
+  uint8_t* dst = sh->pts.as<uint8_t>();
+  for (int t = 0; t < g.N; t++) {
+    const size_t k0 = (size_t)t * g.M + (size_t)g.rank * g.C;
+    const size_t cnt = std::min(g.C, params->h.n > k0 ? params->h.n - k0 : 0);
+    if (cnt) BH_TRY_HIP(hipMemcpyAsync(dst + (size_t)t * g.C * 96, src + k0 * 96, cnt * 96, hipMemcpyDeviceToDevice,
+                                       ctx->stream));
+  }
+  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  *out = sh.get();
+  params->h_shares[key] = std::move(sh);
+  return BH_OK;
+}
+
+// Caller holds params->mu: exclusively with build = true (tables and shares are rebuilt in
+// place), shared otherwise.
+// Plan the 8 multiexps of shard `shard` of `nshards`: scalar ranges, the base ranges they
+// consume and the window table each one uses; with build = true the tables (slices of the
+// Parameters vectors, or a gathered h share) are made resident first.  share: the
+// distributed-H geometry when h comes from the distributed pipeline (then the h job covers
+// the share, not a range).  Device pointers may be null when only tables are prepared.
+bh_status plan_shard(bh_ctx* ctx, const bh_params* params_c, const bh_witness* w, size_t shard, size_t nshards,
+                     const ShareGeom* share, const uint32_t* hbuf, const int32_t* hidx, const int32_t* idx_aaux,
+                     const int32_t* idx_bin, const int32_t* idx_baux, bool build, Job jobs[8]) {
+  bh_params* params = const_cast<bh_params*>(params_c);  // tables are a cache of the CRS
+  const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
+  const uint32_t* inputs = w->inputs.as<uint32_t>();
+  const uint32_t* aux = w->aux.as<uint32_t>();
+  const bool tables = ctx->tables && !ctx->window_override;
+  Job hjob;
+  hjob.srs = &params->h; hjob.sc = ctx->hbuf.as<uint32_t>(); hjob.n = m - 1; hjob.used = m - 1; hjob.out = 0;
+  hjob.is_h = true;
+  if (share) {
+    hjob.presharded = true;
+    hjob.sc = hbuf;
+    hjob.used = share->used();
+    const int c = tables ? table_c_for(share->used()) : 0;
+    bh_srs* sh = nullptr;
+    if (c && !params->h.win_covers(c, 0, m - 1)) {
+      // no full-vector table at this c (the per-rank case): a table over the share's own bases
+      auto it = params->h_shares.find(std::make_tuple(share->N, share->rank, share->L));
+      if (it != params->h_shares.end()) sh = it->second.get();
+      else if (build) {
+        bh_status s = ensure_h_share(ctx, params, *share, &sh);
+        if (s) return s;
+      }
+    }
+    if (sh) {
+      hjob.srs = sh;
+      hjob.n = share->used();
+      hjob.idx = nullptr;  // position p of the share = base p of the gathered vector
+    } else {
+      hjob.n = share->M;
+      hjob.idx = hidx;  // global indices into the full h vector (-1: truncated coefficient)
+    }
+  }
+  auto mk = [](bool g2, const bh_srs* srs, const uint32_t* sc, size_t n, const int32_t* idx, size_t used, int out,
+               const std::vector<uint64_t>* hd, const std::vector<size_t>* pf, size_t boff) {
+    Job j;
+    j.g2 = g2; j.srs = srs; j.sc = sc; j.n = n; j.idx = idx; j.used = used; j.out = out;
+    j.hdens = hd; j.prefix = pf; j.boff = boff;
+    return j;
+  };
+  // G2 first (the longest tail gets the most overlap), then b_g1_aux whose sorted digits are
+  // a copy of b_g2_aux's (so both are ready at the first accumulation for the price of one
+  // sort), h last so the H pipeline has the most slack
+  jobs[0] = mk(true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1, &w->b_aux_density, &w->b_aux_prefix,
+               w->b_in_total);                                                                         // b_g2_aux
+  jobs[1] = mk(false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5, &w->b_aux_density, &w->b_aux_prefix,
+               w->b_in_total);                                                                         // b_g1_aux
+  jobs[2] = mk(false, &params->l, aux, na, nullptr, na, 1, nullptr, nullptr, 0);                       // l
+  jobs[3] = mk(false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3, &w->a_aux_density, &w->a_aux_prefix,
+               ni);                                                                                    // a_aux
+  jobs[4] = hjob;                                                                                      // h
+  jobs[5] = mk(false, &params->a, inputs, ni, nullptr, ni, 2, nullptr, nullptr, 0);                   // a_inputs
+  jobs[6] = mk(false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4, nullptr, nullptr, 0);     // b_g1_inputs
+  jobs[7] = mk(true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0, nullptr, nullptr, 0);      // b_g2_inputs
+  for (int j = 0; j < 8; j++) {
+    Job& J = jobs[j];
+    if (J.presharded) { J.lo = 0; J.hi = J.n; }
+    else shard_range(J.n, shard, nshards, &J.lo, &J.hi);
+    J.table_c = 0;
+    if (J.hi == J.lo) continue;
+    const size_t used = (size_t)((unsigned __int128)J.used * (J.hi - J.lo) / std::max<size_t>(J.n, 1));
+    if (J.idx && !J.prefix && J.presharded) {  // h share over the full vector: any base may be used
+      J.blo = 0; J.bhi = J.srs->n;
+    } else if (j >= 5) {  // the public-input multiexps: tiny, plain windows
+      J.blo = J.boff; J.bhi = J.boff;
+    } else {
+      J.blo = J.boff + dens_before(J, J.lo);
+      J.bhi = J.boff + dens_before(J, J.hi);
+    }
+    if (tables && used >= TABLE_MIN_USED) J.table_c = table_c_for(used);
+  }
+  if (build) {
+    for (int j = 0; j < 8; j++) {
+      const Job& J = jobs[j];
+      if (!J.table_c) continue;
+      bh_status s = ensure_table(ctx, const_cast<bh_srs*>(J.srs), J.table_c, J.blo, J.bhi);
+      if (s) return s;
+    }
+  }
+  return BH_OK;
+}
+
+// would plan_shard(build = true) change anything resident?
+bool plan_needs_build(const bh_params* params, const Job jobs[8], const ShareGeom* share, bool tables) {
+  if (share && tables) {
+    const int c = table_c_for(share->used());
+    const size_t m_1 = params->h.n;
+    if (c && !params->h.win_covers(c, 0, m_1) &&
+        !params->h_shares.count(std::make_tuple(share->N, share->rank, share->L)))
+      return true;
+  }
+  for (int j = 0; j < 8; j++)
+    if (jobs[j].table_c && table_wanted(jobs[j].srs, jobs[j].table_c, jobs[j].blo, jobs[j].bhi)) return true;
+  return false;
+}
+
+// Full-vector tables at the window size of one of nshards shards (bh_params_prepare): every
+// shard's slice is covered, so one device can run all N shards (rehearsal, partials_local).
+bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t na, size_t a_aux_used,
+                              size_t b_aux_used, size_t nshards) {
+  if (!ctx->tables || ctx->window_override) return BH_OK;
+  const size_t N = std::max<size_t>(nshards, 1);
+  bh_status s;
+  auto full = [&](bh_srs* v, size_t used) { return ensure_table(ctx, v, table_c_for(used / N), 0, v->n); };
+  if ((s = full(&params->h, m - 1))) return s;
+  if ((s = full(&params->l, na))) return s;
+  if ((s = full(&params->a, a_aux_used))) return s;
+  if ((s = full(&params->b_g1, b_aux_used))) return s;
+  return full(&params->b_g2, b_aux_used);
+}
+
+// When an exchanger is given (RCCL ranks, or the one-device emulation's virtual ranks) and
+// the rank count qualifies, the H block is distributed (dist_h.h): this rank's h multiexp then
+// covers the share of h it ends with instead of the range [shard*(m-1)/N, ...).
 
 // `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
 // res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
 bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
-                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], const HSource& hsrc = HSource()) {
+                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true) {
   const auto t0 = std::chrono::steady_clock::now();
+  bh_params* mparams = const_cast<bh_params*>(params);
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
   const int L = w->log_m;
   bh_status s;
@@ -322,9 +513,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(ctx->dtmp.alloc((maxn / 64 + 2) * 4));
   BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(maxn / 64 + 2) * 4 + 64));
   BH_TRY_HIP(ctx->dspan.alloc(16 * 4));
-
-  if ((s = prepare_tables(ctx, const_cast<bh_params*>(params), m, na, w->a_aux_total, w->b_aux_total, nshards)))
-    return s;
 
   // ---- error semantics (prover.rs:309-343 order: delta check, then the waits)
   const uint64_t* dens = w->dens.as<uint64_t>();
@@ -375,91 +563,78 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
 
   // ---- the 8 multiexps (prover.rs:233-307)
-  const uint32_t* inputs = w->inputs.as<uint32_t>();
-  const uint32_t* aux = w->aux.as<uint32_t>();
   BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
   int32_t* idx_aaux = ctx->idx3.as<int32_t>();
   int32_t* idx_bin = idx_aaux + na;
   int32_t* idx_baux = idx_bin + ni;
+  // distributed H: this rank ends with its own share of h (dist_h.h), no range split
+  DistH* dh = nullptr;
+  if (ex && dist_h_eligible((int)nshards, L) && nshards >= dist_h_min_ranks()) {
+    if (!ctx->dist) ctx->dist = new DistH();
+    if ((s = dist_h_init(ctx, *ctx->dist, (int)nshards, (int)shard, L))) return s;
+    dh = ctx->dist;
+  }
+  ShareGeom geom;
+  if (dh) {
+    geom.N = dh->N; geom.rank = dh->rank; geom.L = L; geom.M = dh->M; geom.C = dh->C;
+  }
+  const ShareGeom* sg = dh ? &geom : nullptr;
+  const uint32_t* sh_buf = dh ? dh->hbuf.as<uint32_t>() : nullptr;
+  const int32_t* sh_idx = dh ? dh->hidx.as<int32_t>() : nullptr;
+  // The proof reads the Parameters' window tables under a shared lock for its whole duration;
+  // tables it wants but lacks are built first under the exclusive lock (a proof of another
+  // shape may have replaced them).
+  Job jobs[8];
+  std::shared_lock<std::shared_mutex> prd(mparams->mu);
+  if ((s = plan_shard(ctx, params, w, shard, nshards, sg, sh_buf, sh_idx, idx_aaux, idx_bin, idx_baux, false, jobs)))
+    return s;
+  if (may_build && plan_needs_build(params, jobs, sg, ctx->tables && !ctx->window_override)) {
+    prd.unlock();
+    {
+      std::unique_lock<std::shared_mutex> pwr(mparams->mu);
+      if ((s = plan_shard(ctx, params, w, shard, nshards, sg, sh_buf, sh_idx, idx_aaux, idx_bin, idx_baux, true,
+                          jobs)))
+        return s;
+    }
+    prd.lock();
+    if ((s = plan_shard(ctx, params, w, shard, nshards, sg, sh_buf, sh_idx, idx_aaux, idx_bin, idx_baux, false,
+                        jobs)))
+      return s;
+  }
   if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
   if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), sS));
   if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx_baux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
-  struct Job {
-    bool g2;
-    const bh_srs* srs;
-    const uint32_t* sc;
-    size_t n;              // full query length (sharded below)
-    const int32_t* idx;    // density map (already offset into the base vector) or null
-    size_t used;           // density-set scalars (roofline accounting)
-    int out;               // result slot: G1 0..5 / G2 0..1
-    bool is_h = false;     // h: needs the H pipeline
-    bool presharded = false;  // n/idx are this shard's already (distributed H)
-  };
-  // distributed H: this rank ends with its own share of h (dist_h.h), no range split
-  DistH* dh = nullptr;
-  if (hsrc.comm && dist_h_eligible((int)nshards, L) && nshards >= dist_h_min_ranks()) {
-    if (!ctx->dist) ctx->dist = new DistH();
-    if ((s = dist_h_init(ctx, *ctx->dist, (int)nshards, (int)shard, L))) return s;
-    dh = ctx->dist;
-  }
-  const DistH* hshare = hsrc.pre ? hsrc.pre : dh;
-  Job hjob{false, &params->h, ctx->hbuf.as<uint32_t>(), m - 1, nullptr, m - 1, 0, true, false};
-  if (hshare) {
-    const size_t used = hshare->rank == hshare->N - 1 ? hshare->M - 1 : hshare->M;
-    hjob = Job{false, &params->h, hshare->hbuf.as<uint32_t>(), hshare->M, hshare->hidx.as<int32_t>(), used, 0, true,
-               true};
-  }
-  // G2 first (the longest tail gets the most overlap), then b_g1_aux whose sorted digits are
-  // a copy of b_g2_aux's (so both are ready at the first accumulation for the price of one
-  // sort), h last so the H pipeline has the most slack
-  const Job jobs[8] = {
-      {true, &params->b_g2, aux, na, idx_baux, w->b_aux_total, 1},              // b_g2_aux
-      {false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5},             // b_g1_aux
-      {false, &params->l, aux, na, nullptr, na, 1},                             // l
-      {false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3},                // a_aux
-      hjob,                                                                     // h
-      {false, &params->a, inputs, ni, nullptr, ni, 2},                          // a_inputs
-      {false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4},            // b_g1_inputs
-      {true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0},             // b_g2_inputs
-  };
   MsmShape shapes[8];
   bool use_table[8] = {false};
   size_t los[8], his[8];
+  int n_table = 0, n_large = 0;
   for (int j = 0; j < 8; j++) {
-    if (jobs[j].presharded) {
-      los[j] = 0;
-      his[j] = jobs[j].n;
-    } else {
-      shard_range(jobs[j].n, shard, nshards, &los[j], &his[j]);
-    }
+    los[j] = jobs[j].lo;
+    his[j] = jobs[j].hi;
     if (his[j] == los[j]) continue;
-    const size_t used = (size_t)((unsigned __int128)jobs[j].used * (his[j] - los[j]) / std::max<size_t>(jobs[j].n, 1));
     const bh_srs* srs = jobs[j].srs;
-    use_table[j] = srs->win_c && used >= TABLE_MIN_USED;
+    use_table[j] = jobs[j].table_c && srs->win_covers(jobs[j].table_c, jobs[j].blo, jobs[j].bhi);
     shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
                              : msm_shape(his[j] - los[j], ctx->window_override);
     if (use_table[j]) shapes[j].rec = srs->win_rec;
     if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
     else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
+    if (jobs[j].table_c) n_large++;
+    if (use_table[j]) n_table++;
   }
   // ---- H (prover.rs:210-234), device resident.  Where it is enqueued depends on h_mode
   // (below); only h's sort waits for it.
   auto enqueue_h = [&](hipEvent_t after) -> bh_status {
     BH_TRY_HIP(hipStreamWaitEvent(sH, after, 0));
     hipEventRecord(ctx->ev[0], sH);
-    if (hsrc.pre) {  // share computed beforehand
-      hipEventRecord(ctx->ev[1], sH);
-      return BH_OK;
-    }
-    if (dh) {  // three all-to-alls over RCCL, stream-ordered on sH
-      bh_comm* cm = hsrc.comm;
+    if (dh) {  // three all-to-alls (RCCL, or the emulation's device copies), stream-ordered on sH
       const size_t chunk = dh->C, M = dh->M;
-      HExchange ex = [cm, chunk, M](const uint32_t* send, uint32_t* recv, int nvec, hipStream_t st) {
-        return comm_exchange(cm, send, recv, chunk, M, nvec, st);
+      HExchange hx = [ex, chunk, M](const uint32_t* send, uint32_t* recv, int nvec, hipStream_t st) {
+        return ex->exchange(send, recv, chunk, M, nvec, st);
       };
-      bh_status hs = dist_h_run(ctx, *dh, w->abc.as<uint32_t>(), ex, sH);
+      bh_status hs = dist_h_run(ctx, *dh, w->abc.as<uint32_t>(), hx, sH);
       if (hs) return hs;
       hipEventRecord(ctx->ev[1], sH);
       return BH_OK;
@@ -566,7 +741,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     MsmTiming tm;
     tm.ev_acc_begin = jev[2 * j];
     tm.ev_acc_end = jev[2 * j + 1];
-    const uint32_t* bases = use_table[j] ? J.srs->win.as<uint32_t>() : J.srs->pts.as<uint32_t>();
+    const uint32_t* bases = use_table[j] ? J.srs->win_global() : J.srs->pts.as<uint32_t>();
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
@@ -714,6 +889,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ctx->last_timings[7] = (double)g2_pairs;
   ctx->last_timings[8] = (double)g1_adds;
   ctx->last_timings[9] = (double)g2_adds;
+  ctx->last_timings[10] = n_table;
+  ctx->last_timings[11] = n_large;
+  size_t tb = params->h.win.bytes + params->l.win.bytes + params->a.win.bytes + params->b_g1.win.bytes +
+              params->b_g2.win.bytes;
+  for (const auto& kv : params->h_shares) tb += kv.second->win.bytes;
+  ctx->last_timings[12] = (double)tb;
   return BH_OK;
 }
 
@@ -759,25 +940,177 @@ void write_partial(const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], uint8_t* out) 
   for (int i = 0; i < 2; i++) g2_to_uncompressed(jac_to_affine(r2[i]), out + 576 + 192 * i);
 }
 
+// N virtual ranks of one device, one host thread each: the all-to-all as device copies.
+struct LocalGroup {
+  explicit LocalGroup(int n) : N(n), send(n, nullptr), ready(n, nullptr), copied(n, nullptr) {}
+  int N;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  size_t gen = 0;
+  bool aborted = false;
+  std::vector<const uint32_t*> send;
+  std::vector<hipEvent_t> ready, copied;
+  // false if a rank failed (its peers must not wait for it)
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
+    const size_t g = gen;
+    if (++arrived == N) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+      return true;
+    }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
+struct LocalExchanger : Exchanger {
+  LocalGroup* g;
+  int r;
+  LocalExchanger(LocalGroup* gg, int rr) : g(gg), r(rr) {}
+  int rank() const override { return r; }
+  int size() const override { return g->N; }
+  bh_status exchange(const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec, hipStream_t st) override {
+    g->send[r] = send;
+    BH_TRY_HIP(hipEventRecord(g->ready[r], st));
+    if (!g->barrier()) return BH_ERR_HIP;  // every rank's send buffer is final once its event fires
+    for (int p = 0; p < g->N; p++) {
+      if (p != r) BH_TRY_HIP(hipStreamWaitEvent(st, g->ready[p], 0));
+      for (int v = 0; v < nvec; v++)  // chunk r of p's send -> chunk p of my recv
+        BH_TRY_HIP(hipMemcpyAsync(recv + ((size_t)v * M + (size_t)p * C) * 8,
+                                  g->send[p] + ((size_t)v * M + (size_t)r * C) * 8, C * 32, hipMemcpyDeviceToDevice,
+                                  st));
+    }
+    BH_TRY_HIP(hipEventRecord(g->copied[r], st));
+    if (!g->barrier()) return BH_ERR_HIP;
+    // my send buffer is rewritten later on this stream: only after every peer has copied from it
+    for (int p = 0; p < g->N; p++)
+      if (p != r) BH_TRY_HIP(hipStreamWaitEvent(st, g->copied[p], 0));
+    return BH_OK;
+  }
+};
+
+inline int dev_of(const bh_ctx* c) { return c ? c->device : -1; }
+// Parameters and witnesses live in one device's HBM: a context of another device cannot use them
+bool same_device(const bh_ctx* ctx, const bh_params* p, const bh_witness* w) {
+  return (!p || dev_of(p->ctx) == ctx->device) && (!w || dev_of(w->ctx) == ctx->device);
+}
+
+// compute_msms, and on failure wait for whatever it had already enqueued on the context's
+// streams (the next call reuses the same workspaces)
+bh_status compute_msms_sync(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
+                            Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true) {
+  bh_status s = compute_msms(ctx, params, w, shard, nshards, res1, res2, ex, may_build);
+  if (s) ctx_sync_all(ctx);
+  return s;
+}
+
+// N ranks of one device, one context and one host thread each, running exactly the per-rank
+// code of bh_prove_witness_partial_comm with a LocalExchanger in place of RCCL.  With
+// prebuilt = false each rank's tables are built first, rank after rank (a rank must never
+// build while its peers wait for it inside an exchange); the threads themselves never build.
+bh_status run_ranks(const std::vector<bh_ctx*>& ctxs, const std::vector<const bh_params*>& ps, const bh_witness* w,
+                    uint8_t* partials_out, bool build_first) {
+  const int N = (int)ctxs.size();
+  if (build_first) {
+    for (int k = 0; k < N; k++) {
+      bh_ctx* v = ctxs[k];
+      std::lock_guard<std::mutex> vl(v->mu);
+      BH_TRY_HIP(hipSetDevice(v->device));
+      ShareGeom geom;
+      const bool dist = dist_h_eligible(N, w->log_m) && (size_t)N >= dist_h_min_ranks();
+      if (dist) {
+        geom.N = N; geom.rank = k; geom.L = w->log_m; geom.M = w->m / N; geom.C = geom.M / N;
+      }
+      std::unique_lock<std::shared_mutex> pwr(const_cast<bh_params*>(ps[k])->mu);
+      Job jobs[8];
+      bh_status s = plan_shard(v, ps[k], w, (size_t)k, (size_t)N, dist ? &geom : nullptr, nullptr, nullptr, nullptr,
+                               nullptr, nullptr, true, jobs);
+      if (s) return s;
+    }
+  }
+  LocalGroup grp(N);
+  struct EvGuard {
+    LocalGroup& g;
+    ~EvGuard() {
+      for (int k = 0; k < g.N; k++) {
+        if (g.ready[k]) (void)hipEventDestroy(g.ready[k]);
+        if (g.copied[k]) (void)hipEventDestroy(g.copied[k]);
+      }
+    }
+  } guard{grp};
+  for (int k = 0; k < N; k++) {
+    BH_TRY_HIP(hipEventCreateWithFlags(&grp.ready[k], hipEventDisableTiming));
+    BH_TRY_HIP(hipEventCreateWithFlags(&grp.copied[k], hipEventDisableTiming));
+  }
+  std::vector<bh_status> st(N, BH_OK);
+  std::vector<std::thread> th;
+  for (int k = 0; k < N; k++)
+    th.emplace_back([&, k] {
+      bh_ctx* v = ctxs[k];
+      std::lock_guard<std::mutex> vl(v->mu);
+      if (hipSetDevice(v->device) != hipSuccess) { st[k] = BH_ERR_HIP; grp.abort(); return; }
+      LocalExchanger ex(&grp, k);
+      Jac<Fp> r1[6];
+      Jac<bh::Fp2> r2[2];
+      st[k] = compute_msms_sync(v, ps[k], w, (size_t)k, (size_t)N, r1, r2, &ex, false);
+      if (st[k]) { grp.abort(); return; }
+      write_partial(r1, r2, partials_out + (size_t)k * PARTIAL_BYTES);
+    });
+  for (auto& t : th) t.join();
+  for (int k = 0; k < N; k++)
+    if (st[k]) return st[k];
+  return BH_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 bh_status bh_params_prepare(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t nshards) {
   if (!ctx || !params || !w || nshards == 0) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
-  return prepare_tables(ctx, params, w->m, w->num_aux, w->a_aux_total, w->b_aux_total, nshards);
+  std::unique_lock<std::shared_mutex> pwr(params->mu);
+  return prepare_tables_full(ctx, params, w->m, w->num_aux, w->a_aux_total, w->b_aux_total, nshards);
+}
+
+bh_status bh_params_prepare_shard(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
+                                  int distributed_h) {
+  if (!ctx || !params || !w || nshards == 0 || shard >= nshards) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  ShareGeom geom;
+  const bool dist = distributed_h && dist_h_eligible((int)nshards, w->log_m) && nshards >= dist_h_min_ranks();
+  if (dist) {
+    geom.N = (int)nshards; geom.rank = (int)shard; geom.L = w->log_m;
+    geom.M = w->m / nshards; geom.C = geom.M / nshards;
+  }
+  std::unique_lock<std::shared_mutex> pwr(params->mu);
+  Job jobs[8];
+  return plan_shard(ctx, params, w, shard, nshards, dist ? &geom : nullptr, nullptr, nullptr, nullptr, nullptr,
+                    nullptr, true, jobs);
 }
 
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r_in[4],
                            const uint64_t s_in[4], uint8_t proof_out[192]) {
   if (!ctx || !params || !w || !r_in || !s_in || !proof_out) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
   Jac<Fp> r1[6];
   Jac<bh::Fp2> r2[2];
-  bh_status s = compute_msms(ctx, params, w, 0, 1, r1, r2);
+  bh_status s = compute_msms_sync(ctx, params, w, 0, 1, r1, r2);
   if (s) return s;
   const auto t0 = std::chrono::steady_clock::now();
   assemble(vk_of(params), r1, r2, r_in, s_in, proof_out);
@@ -796,11 +1129,12 @@ bh_status bh_shard_range(size_t n, size_t shard, size_t nshards, size_t* lo, siz
 bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard,
                                    size_t nshards, uint8_t partial_out[960]) {
   if (!ctx || !params || !w || !partial_out || nshards == 0 || shard >= nshards) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
   Jac<Fp> r1[6];
   Jac<bh::Fp2> r2[2];
-  bh_status s = compute_msms(ctx, params, w, shard, nshards, r1, r2);
+  bh_status s = compute_msms_sync(ctx, params, w, shard, nshards, r1, r2);
   if (s) return s;
   write_partial(r1, r2, partial_out);
   return BH_OK;
@@ -809,13 +1143,13 @@ bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const b
 bh_status bh_prove_witness_partial_comm(bh_ctx* ctx, const bh_params* params, const bh_witness* w, bh_comm* comm,
                                         uint8_t partial_out[960]) {
   if (!ctx || !params || !w || !comm || !partial_out) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
   Jac<Fp> r1[6];
   Jac<bh::Fp2> r2[2];
-  HSource hs;
-  hs.comm = comm;
-  bh_status s = compute_msms(ctx, params, w, (size_t)comm_rank(comm), (size_t)comm_size(comm), r1, r2, hs);
+  std::unique_ptr<Exchanger> ex = rccl_exchanger(comm);
+  bh_status s = compute_msms_sync(ctx, params, w, (size_t)ex->rank(), (size_t)ex->size(), r1, r2, ex.get());
   if (s) return s;
   write_partial(r1, r2, partial_out);
   return BH_OK;
@@ -823,58 +1157,46 @@ bh_status bh_prove_witness_partial_comm(bh_ctx* ctx, const bh_params* params, co
 
 bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, const bh_witness* w,
                                           size_t nshards, uint8_t* partials_out) {
-  if (!ctx || !params || !w || !partials_out || nshards == 0) return BH_ERR_INVALID_ARGUMENT;
+  if (!ctx || !params || !w || !partials_out || nshards == 0 || nshards > 64) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
   const int N = (int)nshards;
-  std::vector<std::unique_ptr<DistH>> d;
-  if (dist_h_eligible(N, w->log_m)) {
-    // N virtual ranks on this device: the distributed H pipeline with device copies for the
-    // all-to-alls, each rank's share kept for its multiexps below
-    for (int k = 0; k < N; k++) {
-      d.emplace_back(new DistH());
-      bh_status s = dist_h_init(ctx, *d.back(), N, k, w->log_m);
-      if (s) return s;
-    }
-    hipStream_t st = ctx->stream;
-    const size_t C = d[0]->C, M = d[0]->M;
-    auto exchange = [&](bool from_work, int nvec) -> bh_status {
-      for (int dst = 0; dst < N; dst++)
-        for (int src = 0; src < N; src++)
-          for (int v = 0; v < nvec; v++) {
-            const uint32_t* sb = (from_work ? d[src]->work : d[src]->recv).as<uint32_t>();
-            uint32_t* rb = (from_work ? d[dst]->recv : d[dst]->work).as<uint32_t>();
-            BH_TRY_HIP(hipMemcpyAsync(rb + ((size_t)v * M + (size_t)src * C) * 8,
-                                      sb + ((size_t)v * M + (size_t)dst * C) * 8, C * 32, hipMemcpyDeviceToDevice,
-                                      st));
-          }
-      return BH_OK;
-    };
-    bh_status s;
-    const uint32_t* abc = w->abc.as<uint32_t>();
-    for (int k = 0; k < N; k++)
-      if ((s = dist_h_phase1(ctx, *d[k], abc, st))) return s;
-    if ((s = exchange(true, 3))) return s;
-    for (int k = 0; k < N; k++)
-      if ((s = dist_h_phase2(ctx, *d[k], st))) return s;
-    if ((s = exchange(true, 3))) return s;
-    for (int k = 0; k < N; k++)
-      if ((s = dist_h_phase3(ctx, *d[k], st))) return s;
-    if ((s = exchange(false, 1))) return s;
-    for (int k = 0; k < N; k++)
-      if ((s = dist_h_final(ctx, *d[k], st))) return s;
-    BH_TRY_HIP(hipStreamSynchronize(st));
-  }
-  for (int k = 0; k < N; k++) {
-    Jac<Fp> r1[6];
-    Jac<bh::Fp2> r2[2];
-    HSource hs;
-    hs.pre = d.empty() ? nullptr : d[k].get();
-    bh_status s = compute_msms(ctx, params, w, (size_t)k, nshards, r1, r2, hs);
+  while ((int)ctx->vranks.size() < N) {
+    bh_ctx* v = nullptr;
+    bh_status s = bh_ctx_create(ctx->device, &v);
     if (s) return s;
-    write_partial(r1, r2, partials_out + (size_t)k * PARTIAL_BYTES);
+    ctx->vranks.push_back(v);
   }
-  return BH_OK;
+  std::vector<bh_ctx*> ctxs(ctx->vranks.begin(), ctx->vranks.begin() + N);
+  for (bh_ctx* v : ctxs) {
+    v->tables = ctx->tables;
+    v->window_override = ctx->window_override;
+  }
+  // one Parameters for every rank: tables covering every shard (full vectors at the shard's
+  // window size) are built once up front
+  {
+    std::unique_lock<std::shared_mutex> pwr(const_cast<bh_params*>(params)->mu);
+    bh_status s = prepare_tables_full(ctx, const_cast<bh_params*>(params), w->m, w->num_aux, w->a_aux_total,
+                                      w->b_aux_total, nshards);
+    if (s) return s;
+  }
+  std::vector<const bh_params*> ps(N, params);
+  return run_ranks(ctxs, ps, w, partials_out, false);
+}
+
+bh_status bh_prove_witness_partials_ranks(bh_ctx* const* ctxs, const bh_params* const* params, const bh_witness* w,
+                                          size_t nranks, uint8_t* partials_out) {
+  if (!ctxs || !params || !w || !partials_out || nranks == 0 || nranks > 64) return BH_ERR_INVALID_ARGUMENT;
+  std::vector<bh_ctx*> cs(ctxs, ctxs + nranks);
+  std::vector<const bh_params*> ps(params, params + nranks);
+  for (size_t k = 0; k < nranks; k++) {
+    if (!cs[k] || !ps[k] || cs[k]->device != cs[0]->device || !same_device(cs[k], ps[k], w))
+      return BH_ERR_INVALID_ARGUMENT;
+    for (size_t j = 0; j < k; j++)
+      if (cs[j] == cs[k]) return BH_ERR_INVALID_ARGUMENT;  // one context per rank
+  }
+  return run_ranks(cs, ps, w, partials_out, true);
 }
 
 bh_status bh_vk_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written) {
@@ -950,7 +1272,14 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
 
 bh_status bh_last_timings(const bh_ctx* ctx, double out[10]) {
   if (!ctx || !out) return BH_ERR_INVALID_ARGUMENT;
-  memcpy(out, ctx->last_timings, sizeof ctx->last_timings);
+  memcpy(out, ctx->last_timings, 10 * sizeof(double));
+  return BH_OK;
+}
+
+bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n) {
+  if (!ctx || (n && !out)) return BH_ERR_INVALID_ARGUMENT;
+  const size_t have = sizeof ctx->last_timings / sizeof(double);
+  for (size_t i = 0; i < n; i++) out[i] = i < have ? ctx->last_timings[i] : 0.0;
   return BH_OK;
 }
 

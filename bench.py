@@ -47,8 +47,6 @@ def parse():
     ap.add_argument("--cpu-1t-log-constraints", type=int, default=12, help="1-thread CPU sample (0: skip)")
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
     ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
-    ap.add_argument("--exchange", default="rccl",
-                    help="partial-sum exchange: rccl (library-driven RCCL all-gather over xGMI) or gloo (CPU rehearsal)")
     return ap.parse_args()
 
 
@@ -99,18 +97,25 @@ def cpu_baseline(bh, ctx, log_c, log_c_1t):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import bh_launch  # pure Python: loads no HIP library
+    try:
+        world, rank, local, spawn = bh_launch.rank_env(args.gpus)
+    except bh_launch.LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr)
+        sys.exit(2)
+    if spawn:
+        # plain `python bench.py --gpus N`: start the N rank processes (one per GPU, LOCAL_RANK =
+        # device) before this parent touches HIP, and exit with the first failing rank's code
+        rc = bh_launch.spawn_ranks(world, [os.path.abspath(__file__)] + sys.argv[1:])
+        sys.exit(rc if rc >= 0 else 128 - rc)
     import bellman_hip as bh
 
-    # torch.distributed is used for CPU-side rendezvous only (gloo): torch bundles its own
-    # HIP runtime, so the GPU work and the RCCL exchange are driven by libbellman_hip.
-    dist = None
-    device = local % max(1, bh.device_count())  # rehearsal: several ranks may share one card
+    device = local
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
+        ndev = bh.device_count()
+        if ndev < world:
+            print(f"bench.py rank {rank}: --gpus {world} needs {world} devices, HIP sees {ndev}", file=sys.stderr)
+            sys.exit(3)
     k = args.log_constraints
     rounds = (1 << (k - 1)) - 1
     n_constraints = 2 * rounds + 2
@@ -129,48 +134,44 @@ def main():
     t_tables = time.time() - t0
     r, s = 27134, 17146
     vk = params.vk_bytes()
-    comm = None
-    exchange = args.exchange
-    if world > 1 and exchange == "rccl":
-        obj = [bh.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        try:
-            comm = bh.Comm(ctx, obj[0], world, rank)
-        except bh.SynthesisError as e:
-            print(f"rank {rank}: RCCL communicator failed ({e}); exchanging over gloo", file=sys.stderr)
-            exchange = "gloo-fallback"
-        ok = [comm is not None]
-        allok = [None] * world
-        dist.all_gather_object(allok, ok[0])
-        if not all(allok):
-            if comm is not None:
-                comm.close()
-                comm = None
-            exchange = "gloo-fallback"
+    comm, rccl = None, None
+    if world > 1:
+        # RCCL communicator over xGMI: the unique id travels through a rendezvous file, every
+        # other byte through RCCL.  Any failure ends this rank (and the launcher the run).
+        rdzv = bh_launch.rendezvous_dir()
+        if rank == 0:
+            uid = bh.Comm.unique_id()
+            bh_launch.publish(rdzv, "uid", uid)
+        else:
+            uid = bh_launch.wait_for(rdzv, "uid", timeout=600)
+        comm = bh.Comm(ctx, uid, world, rank)
+        if rank == 0:
+            bh_launch.cleanup(rdzv)
+        n_seen, r_seen, d_seen = comm.info()
+        if (n_seen, r_seen, d_seen) != (world, rank, device):
+            print(f"bench.py rank {rank}: RCCL reports ranks={n_seen} rank={r_seen} device={d_seen}, "
+                  f"expected {world}/{rank}/{device}", file=sys.stderr)
+            sys.exit(4)
+        recs = comm.allgather_bytes(json.dumps([rank, device, os.getpid()]).encode().ljust(64))
+        rccl = {"ranks": n_seen, "devices": [json.loads(x.decode().strip())[1] for x in recs]}
+        if len(set(rccl["devices"])) != world:
+            print(f"bench.py: ranks share devices {rccl['devices']}", file=sys.stderr)
+            sys.exit(4)
 
     def step():
         if world == 1:
             return bh.prove_witness(ctx, params, witness, r, s)
-        if comm is not None:  # H block distributed over the ranks (RCCL all-to-alls) for N >= 4
-            part = comm.prove_partial(ctx, params, witness)
-        else:
-            part = bh.prove_witness_partial(ctx, params, witness, rank, world)
-        if comm is not None:
-            parts = comm.allgather(part)  # ncclAllGather over xGMI
-        else:
-            import torch
-            t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
-            gathered = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(gathered, t)
-            parts = b"".join(bytes(g.numpy().tobytes()) for g in gathered)
+        # this rank's share of every multiexp (H block distributed over RCCL for N >= 4),
+        # the 960-byte partial records all-gathered over RCCL, rank 0 sums and assembles
+        parts = comm.allgather(comm.prove_partial(ctx, params, witness))
         if rank == 0:
             return bh.proof_from_partials(vk, parts, world, r, s)
         return None
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
         ctx.synchronize()
+        if comm is not None:
+            comm.allreduce_max(0.0)
 
     ref = None
     for _ in range(args.warmup):
@@ -187,15 +188,14 @@ def main():
             timings.append(ctx.last_timings())
     barrier()
     elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    per_rank_ms = None
+    if comm is not None:
+        mine = elapsed * 1000.0 / args.steps
+        per_rank_ms = [round(json.loads(x.decode().strip()), 3)
+                       for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(32))]
+        elapsed = comm.allreduce_max(elapsed)
     if rank != 0:
-        if comm is not None:
-            comm.close()
-        dist.destroy_process_group()
+        comm.close()
         return
     ms = elapsed * 1000.0 / args.steps
     value = n_constraints * args.steps / elapsed
@@ -229,8 +229,9 @@ def main():
             "mad_u64_tps": round(madd_rate * MADS_PER_G1_MADD / 1e3, 2) if madd_rate else None,
             "mad_u64_frac": round(madd_rate * MADS_PER_G1_MADD / 1e3 / MAD_U64_PEAK_TPS, 4) if madd_rate else None,
             "mad_u64_peak_tps": MAD_U64_PEAK_TPS, "mad_u64_peak_source": "tools/microbench/madbench.hip"}
+    # CPU baseline: rank 0 of a 1-GPU run only (a bounded sample; see cpu_baseline)
     base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints)
-            if args.cpu_baseline else None)
+            if args.cpu_baseline and world == 1 else None)
     out = {
         "metric": "Groth16 constraints/sec, BLS12-381, 2^22-constraint R1CS",
         "value": round(value, 1),
@@ -246,7 +247,9 @@ def main():
         "data": "synthetic MiMC-chain witness (splitmix64 seed 7), device-generated CRS (alpha=6,beta=24,gamma=6,delta=24,tau=2)",
         "config": {"workload": f"C3: full create_proof after synthesis, MiMC chain R={rounds}",
                    "constraints": n_constraints, "log_domain": k, "parallelism": f"msm-shard{world}",
-                   "exchange": exchange if world > 1 else None},
+                   "exchange": "rccl" if world > 1 else None},
+        "rccl": rccl,
+        "per_rank_ms_per_step": per_rank_ms,
         "roofline": roof,
         "valu_roofline": valu,
         "end_to_end": {"value": round(n_constraints / (t_wit + ms / 1e3), 1), "unit": "constraints/s",
@@ -261,11 +264,9 @@ def main():
                     "srs_window_tables": round(t_tables, 2) if args.tables else None},
         "proof_sha_prefix": ref.hex()[:32] if ref else None,
     }
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
     if comm is not None:
         comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -80,8 +80,9 @@ bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domai
 bh_status bh_ctx_set_window(bh_ctx* ctx, int c);
 /* Prover SRS window tables (default 1 = on): for each large query of the Parameters the
  * prover keeps T[i*W + w] = 2^(c*w) * P_i resident in HBM (built once per Parameters,
- * ~31 GB at 2^22 constraints, skipped when HBM is short) so that all digit windows share
- * one bucket set and c can grow.  Results never depend on it. */
+ * ~42 GB at 2^22 constraints on one GPU, 1/N of that per rank of an N-GPU run; skipped, with
+ * a message on stderr, when HBM is short) so that all digit windows share one bucket set and
+ * c can grow.  Results never depend on it. */
 bh_status bh_ctx_set_tables(bh_ctx* ctx, int enable);
 
 /* ---- bases (Source over Arc<Vec<G1Affine|G2Affine>>) */
@@ -137,6 +138,11 @@ bh_status bh_witness_free(bh_witness* w);
 /* Build now (instead of inside the first proof) the window tables that proofs of witnesses
  * shaped like w, split over nshards GPUs, will use.  Optional. */
 bh_status bh_params_prepare(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t nshards);
+/* The same for ONE shard: only the slices of the query vectors that shard `shard` of
+ * `nshards` consumes (and, with distributed_h, its gathered share of the h vector), so that
+ * a rank of a multi-GPU run holds and builds 1/nshards of the tables.  Optional. */
+bh_status bh_params_prepare_shard(bh_ctx* ctx, bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
+                                  int distributed_h);
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r[4],
                            const uint64_t s[4], uint8_t proof_out[192]);
 
@@ -161,6 +167,13 @@ bh_status bh_comm_init(bh_ctx* ctx, const uint8_t id[128], int nranks, int rank,
 /* all ranks' records, rank order: all_out holds nranks * BH_PARTIAL_BYTES bytes */
 bh_status bh_comm_allgather_partials(bh_comm* c, const uint8_t* partial, uint8_t* all_out);
 bh_status bh_comm_destroy(bh_comm* c);
+/* every rank's nbytes-byte host record, rank order, into all_out (nranks * nbytes) */
+bh_status bh_comm_allgather(bh_comm* c, const uint8_t* in, size_t nbytes, uint8_t* all_out);
+/* max over ranks of *inout (in place, every rank); returns once every rank has called it,
+ * so it is also the barrier around a timed region */
+bh_status bh_comm_allreduce_max(bh_comm* c, double* inout);
+/* what RCCL reports for the communicator: out = {rank count, this rank, HIP device id} */
+bh_status bh_comm_info(const bh_comm* c, int out[3]);
 /* This rank's partial record (rank/nranks from the communicator).  For nranks a power of two
  * in [BH_DIST_H_MIN (default 4), 16] and m >= 2*nranks^2 the H block is distributed instead
  * of replicated: every NTT is a local m/nranks-point NTT plus one ncclSend/ncclRecv
@@ -169,11 +182,17 @@ bh_status bh_comm_destroy(bh_comm* c);
  * identical to bh_prove_witness_partial(ctx, params, w, rank, nranks, ...). */
 bh_status bh_prove_witness_partial_comm(bh_ctx* ctx, const bh_params* params, const bh_witness* w, bh_comm* comm,
                                         uint8_t partial_out[960]);
-/* All nshards partial records computed on this one device, the distributed H pipeline run
- * with nshards virtual ranks and device copies for its all-to-alls (rehearsal and tests of
- * the multi-GPU algorithm).  partials_out: nshards * BH_PARTIAL_BYTES. */
+/* All nshards partial records computed on this one device by nshards virtual ranks: each a
+ * context and a host thread of its own running the per-rank code of
+ * bh_prove_witness_partial_comm, with device copies in place of the RCCL all-to-alls
+ * (rehearsal and tests of the multi-GPU algorithm).  partials_out: nshards * BH_PARTIAL_BYTES. */
 bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, const bh_witness* w,
                                           size_t nshards, uint8_t* partials_out);
+/* The same with caller-provided ranks of one device: ctxs[k] and params[k] are rank k's context
+ * and Parameters (e.g. loaded per rank and prepared with bh_params_prepare_shard, exactly as
+ * the processes of a multi-GPU run hold them); the witness is shared. */
+bh_status bh_prove_witness_partials_ranks(bh_ctx* const* ctxs, const bh_params* const* params, const bh_witness* w,
+                                          size_t nranks, uint8_t* partials_out);
 bh_status bh_ctx_synchronize(bh_ctx* ctx);
 int bh_device_count(void);
 
@@ -186,6 +205,13 @@ bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness
  * bh_chain_witness(seed) == bh_chain_witness_preimage(seed, seed + 1). */
 bh_status bh_chain_witness_preimage(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t preimage_seed,
                                     bh_witness** out);
+/* The chain's ProvingAssignment on the host, in exactly the layouts bh_prove takes (the
+ * drop-in path a Rust caller uses after synthesis): sizes = {constraints, inputs, aux};
+ * a, b, c: constraints x 4 u64 Montgomery; inputs/aux Montgomery; density bit words. */
+bh_status bh_chain_sizes(size_t rounds, size_t out[3]);
+bh_status bh_chain_assignment(size_t rounds, uint64_t seed, uint64_t preimage_seed, uint64_t* a, uint64_t* b,
+                              uint64_t* c, uint64_t* inputs, uint64_t* aux, uint64_t* a_aux_density,
+                              uint64_t* b_input_density, uint64_t* b_aux_density);
 bh_status bh_chain_params(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t alpha, uint64_t beta, uint64_t gamma,
                           uint64_t delta, uint64_t tau, bh_params** out);
 /* Parameters::write of device-resident params (for parity tests; host copy). */
@@ -196,6 +222,10 @@ bh_status bh_params_write(const bh_params* p, uint8_t* out, size_t cap, size_t* 
  * [3] G1 accumulation launches, [4] G1 (base, scalar) pairs, [5] G2 accumulation ms,
  * [6] G2 launches, [7] G2 pairs, [8] G1 mixed additions, [9] G2 mixed additions */
 bh_status bh_last_timings(const bh_ctx* ctx, double out[10]);
+/* bh_last_timings' fields followed by [10] large multiexps that used a window table,
+ * [11] large multiexps (those a table would serve), [12] window-table bytes resident for the
+ * Parameters; n entries are written (missing ones 0). */
+bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
 
 #ifdef __cplusplus
 }

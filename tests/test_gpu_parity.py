@@ -483,3 +483,20 @@ def test_fft_composition(ctx, logm):
         getattr(d, first)()
         getattr(d, second)()
         assert list(d.into_coeffs()) == v, (first, second)
+
+
+@pytest.mark.parametrize("rounds", [15, (1 << 15) - 1])
+def test_bh_prove_from_host_buffers(ctx, golden, rounds):
+    """bh_prove, the drop-in entry point: the ProvingAssignment as
+    host buffers in bls12_381's layouts (a/b/c/assignments as 4-limb Montgomery Fr, densities
+    as bitvec words) straight to the 192-byte proof.  Equals the golden proof (r15) and the
+    device-resident-witness proof (2^16 constraints)."""
+    bh = _bh()
+    params = bh.Parameters.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    proof = bh.prove(ctx, params, asg, 27134, 17146)
+    if rounds == 15:
+        fx = [f for f in golden["proofs"] if f["name"] == "mimc_chain_r15"][0]
+        assert proof.hex() == fx["proof"]
+    assert proof == bh.prove_witness(ctx, params, bh.Witness.chain(ctx, rounds), 27134, 17146)
+    assert bh.prove(ctx, params, asg, 27134, 17146) == proof  # buffers reused
