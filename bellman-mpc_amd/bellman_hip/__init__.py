@@ -122,6 +122,7 @@ def _load():
         "bh_last_stats": (I, [P, P, S]),
         "bh_prove_witness_partials_ranks": (I, [P, P, P, S, P]),
         "bh_chain_sizes": (I, [S, P]),
+        "bh_rehearse_rank": (I, [P, P, P, S, S, P]),
         "bh_chain_assignment": (I, [S, U64, U64, P, P, P, P, P, P, P, P]),
         "bh_comm_allreduce_max": (I, [P, P]),
         "bh_comm_info": (I, [P, P]),
@@ -147,7 +148,7 @@ EXPORTED_SYMBOLS = [
     "bh_comm_destroy", "bh_ctx_synchronize", "bh_device_count", "bh_ctx_set_tables", "bh_params_prepare",
     "bh_chain_witness_preimage", "bh_prove_witness_partial_comm", "bh_prove_witness_partials_local",
     "bh_comm_allgather", "bh_comm_allreduce_max", "bh_comm_info", "bh_params_prepare_shard", "bh_last_stats",
-    "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment",
+    "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
 ]
 PARTIAL_BYTES = 960
 
@@ -662,6 +663,13 @@ def prove_witness_partials_ranks(ctxs, params_list, witness):
     out = np.zeros(n * PARTIAL_BYTES, dtype=np.uint8)
     _check(_lib.bh_prove_witness_partials_ranks(ca, pa, witness.h, n, _ptr(out)), "partials_ranks")
     return out.tobytes()
+
+
+def rehearse_rank(ctx, params, witness, rank, nranks):
+    """Rank `rank` of an nranks-GPU run on this device (bh_rehearse_rank): host ms of its proof."""
+    ms = ctypes.c_double()
+    _check(_lib.bh_rehearse_rank(ctx.h, params.h, witness.h, rank, nranks, ctypes.byref(ms)), "rehearse_rank")
+    return ms.value
 
 
 def proof_from_partials(vk_bytes, partials, nshards, r, s):

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 
 #include "api_internal.h"
 #include "dist_h.h"
@@ -466,6 +467,26 @@ bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, 
   }
   return BH_OK;
 }
+HostPool& ctx_pool(bh_ctx* ctx) {
+  if (!ctx->pool) {
+    // memcpy workers for the staging ring: enough to outrun PCIe, few enough for a shared box
+    const unsigned hc = std::thread::hardware_concurrency();
+    ctx->pool.reset(new HostPool((int)std::max(1u, std::min(7u, hc ? hc - 1 : 1u))));
+  }
+  return *ctx->pool;
+}
+
+bh_status upload_fr_staged(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst,
+                           hipStream_t st) {
+  if (padded > n) BH_TRY_HIP(hipMemsetAsync(dst + n * 8, 0, (padded - n) * 32, st));
+  if (n) {
+    BH_TRY_HIP(ctx->ring.copy(ctx_pool(ctx), dst, host, n * 32, st));
+    launch_fr_convert(dst, dst, n, conv_const(FrConv::TO_DEV), 0, st);
+    BH_TRY_HIP(hipGetLastError());
+  }
+  return BH_OK;
+}
+
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host) {
   if (!n) return BH_OK;
   launch_fr_convert(src, src, n, conv_const(FrConv::FROM_DEV), 1, ctx->stream);
@@ -572,7 +593,11 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   BH_TRY_HIP(hipSetDevice(device));
   bh_ctx* c = new bh_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return BH_ERR_HIP;
+  }
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { delete c; return BH_ERR_HIP; }
   // side streams (sorts, H pipeline, reduction tails) at high priority; BH_SIDE_PRIORITY=0
@@ -610,6 +635,11 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   ctx->vranks.clear();
   (void)hipSetDevice(ctx->device);
   ctx_sync_all(ctx);  // nothing may still read the workspaces released below
+  if (ctx->h2d) (void)hipStreamSynchronize(ctx->h2d);
+  ctx->ring.release();
+  ctx->pool.reset();
+  delete ctx->dropin;
+  ctx->dropin = nullptr;
   ctx->g1ws.release();
   ctx->g2ws.release();
   for (auto& w : ctx->pw1) w.release();
@@ -621,6 +651,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
   if (ctx->host_counts) (void)hipHostFree(ctx->host_counts);
   (void)hipStreamDestroy(ctx->stream);
+  if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream4);

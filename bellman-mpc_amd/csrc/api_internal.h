@@ -13,6 +13,7 @@
 #include "host_arith.h"
 #include "msm.h"
 #include "ntt.h"
+#include "staging.h"
 
 namespace bh {
 
@@ -153,6 +154,12 @@ struct bh_ctx {
                                     // [16,32) its continuation span (max_span)
   bh::DevBuf dspan;                 // device words for max_span
   std::vector<bh_ctx*> vranks;      // bh_prove_witness_partials_local: the virtual ranks' contexts
+  // host -> device staging of caller buffers (bh_prove, bh_witness_upload): H2D copy stream,
+  // pinned ring, memcpy threads; dropin = the device witness bh_prove reuses call after call
+  hipStream_t h2d = nullptr;
+  bh::H2DRing ring;
+  std::unique_ptr<bh::HostPool> pool;
+  bh_witness* dropin = nullptr;
   std::mutex mu;
 };
 
@@ -173,6 +180,9 @@ bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, co
 bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
                         const int32_t* d_idx, Jac<Fp2>* out, float* acc_ms);
 bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst);
+// the same through the context's pinned staging ring, enqueued on st (caller holds ctx->mu)
+bh_status upload_fr_staged(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst, hipStream_t st);
+bh::HostPool& ctx_pool(bh_ctx* ctx);
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
 bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,

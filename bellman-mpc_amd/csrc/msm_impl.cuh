@@ -75,13 +75,14 @@ __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_
   return v;
 }
 
-// Level k of a segmented tree reduction over the continuation partials of each
-// bucket (a bucket spanning segments s_first..s_last owns conts[s_first+1..s_last]).
-// After levels 0..K-1, conts[s_first+1] holds their sum.
-template <class C>
-__global__ void __launch_bounds__(256) k_cont_tree(const uint32_t* cont_bucket, const uint32_t* counts,
-                                                   const uint32_t* offsets, uint32_t nbt, uint32_t S, int level,
-                                                   typename C::P* conts) {
+// Level `stride` = F^k of an F-ary tree over each bucket's continuation partials
+// conts[s_first+1 .. s_last]: node j (j = s - s_first - 1, a multiple of F*stride) adds the
+// partials at j + i*stride, i = 1..F-1 (F-1 serial additions per level instead of one per
+// level of the binary tree).  After the levels with stride < span, conts[s_first+1] holds the sum.
+template <class C, int F>
+__global__ void __launch_bounds__(256) k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
+                                                    const uint32_t* offsets, uint32_t nbt, uint32_t S,
+                                                    uint32_t stride, typename C::P* conts) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t E = offsets[nbt];
   if ((size_t)s * S >= E) return;
@@ -91,27 +92,59 @@ __global__ void __launch_bounds__(256) k_cont_tree(const uint32_t* cont_bucket, 
   const uint32_t s_first = off / S;
   const uint32_t ncont = (off + counts[b] - 1) / S - s_first;
   const uint32_t j = s - s_first - 1;
-  const uint32_t half = 1u << level;
-  if ((j & ((half << 1) - 1)) != 0 || j + half >= ncont) return;
-  store_point<C>(&conts[s], C::add(load_point<C>(&conts[s]), load_point<C>(&conts[s + half])));
+  if (j % (stride * F) != 0 || j + stride >= ncont) return;
+  typename C::P acc = load_point<C>(&conts[s]);
+  for (int i = 1; i < F; i++)
+    if (j + i * stride < ncont) acc = C::add(acc, load_point<C>(&conts[s + i * stride]));
+  store_point<C>(&conts[s], acc);
 }
 
-// The same fold for buckets spanning at most CONT_SEQ_MAX segments, one thread per bucket:
-// conts[s_first+1] += conts[s_first+2] + ... + conts[s_last]
-constexpr size_t CONT_SEQ_MAX = 24;
-template <class C>
+// longest span folded by the Q-thread kernel below; longer ones take the 4-ary tree.  The
+// tree's levels are full-grid launches: beside a running accumulation they cost more than a
+// sequential fold of ~16 partials (N = 8 rehearsal at 2^22: 13.4 ms per rank with 4, 10.7 ms
+// with 24).  BH_CONT_SEQ_MAX: A/B experiments.
+inline size_t cont_seq_max() {
+  static const size_t v = [] {
+    const char* e = getenv("BH_CONT_SEQ_MAX");
+    return e ? (size_t)atol(e) : (size_t)64;
+  }();
+  return v;
+}
+
+// The same fold for buckets spanning at most cont_seq_max() segments, Q threads per bucket:
+// thread q of bucket b sums the partials i = q, q+Q, q+2Q, ... of conts[s_first+1 ..
+// s_last], then the Q sums meet in LDS (log2(Q) more additions), so a bucket spanning 16
+// segments costs 4 + 2 serial additions instead of 15.  The tails are VALU-bound chains
+// on a small fraction of the SIMDs: serial depth is their latency.
+template <class C, int Q>
 __global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t nbt,
                                                   uint32_t S, typename C::P* conts) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbt) return;
-  const uint32_t cnt = counts[b];
-  if (cnt == 0) return;
-  const uint32_t off = offsets[b];
-  const uint32_t s_first = off / S, s_last = (off + cnt - 1) / S;
-  if (s_last < s_first + 2) return;
-  typename C::P acc = load_point<C>(&conts[s_first + 1]);
-  for (uint32_t sg = s_first + 2; sg <= s_last; sg++) acc = C::add(acc, load_point<C>(&conts[sg]));
-  store_point<C>(&conts[s_first + 1], acc);
+  extern __shared__ uint4 lds_raw[];
+  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t b = gid / Q, q = gid % Q;
+  uint32_t s_first = 0, ncont = 0;
+  if (b < nbt) {
+    const uint32_t cnt = counts[b];
+    if (cnt) {
+      const uint32_t off = offsets[b];
+      s_first = off / S;
+      ncont = (off + cnt - 1) / S - s_first;  // partials conts[s_first+1 .. s_first+ncont]
+    }
+  }
+  typename C::P acc = C::identity();
+  if (ncont >= 2)
+    for (uint32_t i = q; i < ncont; i += Q) acc = C::add(acc, load_point<C>(&conts[s_first + 1 + i]));
+  store_point<C>(&lds[threadIdx.x], acc);
+  __syncthreads();
+  for (uint32_t h = Q / 2; h > 0; h >>= 1) {
+    if (q < h && ncont >= 2) {
+      acc = C::add(acc, load_point<C>(&lds[threadIdx.x + h]));
+      store_point<C>(&lds[threadIdx.x], acc);
+    }
+    __syncthreads();
+  }
+  if (q == 0 && ncont >= 2) store_point<C>(&conts[s_first + 1], acc);
 }
 
 // Bucket reduction: thread (w, t) sums its L buckets by parts
@@ -173,42 +206,13 @@ __global__ void __launch_bounds__(256) k_sum_tree(const typename C::P* in, uint3
   }
 }
 
-// The accumulate kernel needs E; it reads it from offsets[nbt] on device.
-template <class C>
-__global__ void __launch_bounds__(256) k_accumulate_dev(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
-                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
-                                                        typename C::P* bucket_sums, typename C::P* conts,
-                                                        uint32_t* cont_bucket) {
-  const uint32_t E = offsets[nbt];
-  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t pos0 = seg * S;
-  if (pos0 >= E) return;
-  const uint32_t end = min(pos0 + S, E);
-  uint32_t b = find_bucket(offsets, nbt, pos0);
-  uint32_t next = offsets[b + 1];
-  bool started_here = offsets[b] >= pos0;
-  cont_bucket[seg] = started_here ? 0xffffffffu : b;
-  typename C::P acc = C::identity();
-  for (uint32_t j = pos0; j < end; j++) {
-    if (j == next) {
-      if (started_here) store_point<C>(&bucket_sums[b], acc);
-      else store_point<C>(&conts[seg], acc);
-      b++;
-      while (offsets[b + 1] <= j) b++;
-      next = offsets[b + 1];
-      started_here = true;
-      acc = C::identity();
-    }
-    const typename C::A a = load_base<C>(bases, entries[j], rec);
-    acc = C::madd(acc, a);
-  }
-  if (started_here) store_point<C>(&bucket_sums[b], acc);
-  else store_point<C>(&conts[seg], acc);
-}
-
-// Same accumulation with the next entry's affine base prefetched global -> LDS by
+// Bucket accumulation: thread `seg` adds the bases of sorted entries [seg*S, seg*S + S) into
+// their buckets (XYZZ mixed additions), storing a bucket's sum when the bucket ends inside the
+// segment, or its continuation partial (conts[seg]) when the bucket started in an earlier
+// segment.  The next entry's affine base is prefetched global -> LDS by
 // global_load_lds_dwordx4 (no VGPR cost) while the current mixed addition runs: each wave
 // owns NQ x 64 x 16 B of LDS, lane l's base occupying slot l of each of the NQ rows.
+// (A register-load variant without the prefetch measured slower and was removed.)
 template <class C>
 __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
@@ -272,15 +276,6 @@ __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, 
   else store_point<C>(&conts[seg], acc);
 }
 
-// BH_ACC_PREFETCH=0 selects the register-load variant (A/B measurements only)
-inline int accumulate_variant() {
-  static int v = [] {
-    const char* e = getenv("BH_ACC_PREFETCH");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 // Segment length S so that the accumulation grid is exactly ROUNDS full waves of
 // resident workgroups (occupancy from the compiled kernel, CUs from the device): a
 // partial last round would leave most of the chip idle for its whole duration.
@@ -290,7 +285,7 @@ void fit_segments(MsmShape& sh, size_t n) {
     int dev = 0, cus = 256, blocks = 1;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* k = accumulate_variant() ? (const void*)k_accumulate_pf<C> : (const void*)k_accumulate_dev<C>;
+    const void* k = (const void*)k_accumulate_pf<C>;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
     return (size_t)cus * (size_t)blocks * 256;
   }();
@@ -456,14 +451,9 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
-    if (accumulate_variant())
-      hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
-                         ws.cont_bucket);
-    else
-      hipLaunchKernelGGL(k_accumulate_dev<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
-                         ws.cont_bucket);
+    hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                       ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
+                       ws.cont_bucket);
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
   }
   return hipGetLastError();
@@ -486,16 +476,19 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   // log-depth continuation fix-up: a bucket can span up to segs segments
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
-  if (max_span >= 0 && span <= CONT_SEQ_MAX) {
-    // short spans (the common case, known from the sort): one thread per bucket folds its
-    // continuation partials in sequence -- one launch instead of log2(span) full-grid levels
+  if (max_span >= 0 && span <= cont_seq_max()) {
+    // short spans (known from the sort): Q threads per bucket fold its continuation partials
+    // -- one launch, about span/Q + log2(Q) serial additions
+    constexpr int Q = 4;
+    constexpr uint32_t B = sizeof(typename C::P) > 256 ? 128 : 256;  // LDS: B points
     if (span >= 2)
-      hipLaunchKernelGGL(k_cont_seq<C>, dim3(msm_blocks_for(nbt, 256)), dim3(256), 0, st, ws.counts, ws.offsets,
-                         (uint32_t)nbt, (uint32_t)sh.S, ws.conts);
+      hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nbt * Q, B)), dim3(B), B * sizeof(typename C::P), st,
+                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, ws.conts);
   } else {
-    for (int level = 0; ((size_t)1 << level) < span; level++)
-      hipLaunchKernelGGL(k_cont_tree<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
-                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, level, ws.conts);
+    // a bucket owns at most span continuation partials: 4-ary tree levels, 3 serial additions each
+    for (size_t stride = 1; stride < span; stride *= 4)
+      hipLaunchKernelGGL((k_cont_treeF<C, 4>), dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
+                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, (uint32_t)stride, ws.conts);
   }
   const uint32_t T = (uint32_t)(sh.NB / sh.L);
   const size_t total = (size_t)sh.Wb * T;

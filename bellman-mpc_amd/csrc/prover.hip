@@ -93,6 +93,93 @@ inline size_t popcount_words(const std::vector<uint64_t>& w, size_t nbits) {
   return c;
 }
 
+// ---- the complete assignment on the device (prover.rs:206-231 hands create_proof host
+// Vecs).  witness_host: argument checks, sizes, host copies of the density maps and their
+// prefix counts, device buffers; witness_device: the staged copies and format conversions on
+// stream st, in the order the prover needs them -- density maps, inputs, aux (then up stage
+// 1: every multiexp's sort can start), a, b, c (stage 2: the H block can start).
+bh_status witness_host(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                       size_t nc, const uint64_t* inputs, size_t ni, const uint64_t* aux, size_t na,
+                       const uint64_t* a_aux_density, const uint64_t* b_input_density,
+                       const uint64_t* b_aux_density) {
+  if ((nc && (!a || !b || !c)) || (ni && !inputs) || (na && !aux)) return BH_ERR_INVALID_ARGUMENT;
+  if ((na && (!a_aux_density || !b_aux_density)) || (ni && !b_input_density)) return BH_ERR_INVALID_ARGUMENT;
+  size_t m;
+  uint32_t L;
+  bh_status s = bh_domain_size(nc, &m, &L);  // EvaluationDomain::from_coeffs, prover.rs:211-213
+  if (s) return s;
+  w->ctx = ctx;
+  w->num_constraints = nc; w->m = m; w->log_m = (int)L; w->num_inputs = ni; w->num_aux = na;
+  BH_TRY_HIP(w->abc.alloc(3 * m * 32));
+  BH_TRY_HIP(w->inputs.alloc(std::max<size_t>(ni, 1) * 32));
+  BH_TRY_HIP(w->aux.alloc(std::max<size_t>(na, 1) * 32));
+  w->a_aux_words = (na + 63) / 64;
+  w->b_in_words = (ni + 63) / 64;
+  w->b_aux_words = (na + 63) / 64;
+  w->a_aux_density.assign(a_aux_density ? a_aux_density : nullptr, a_aux_density ? a_aux_density + w->a_aux_words : nullptr);
+  w->b_input_density.assign(b_input_density ? b_input_density : nullptr,
+                            b_input_density ? b_input_density + w->b_in_words : nullptr);
+  w->b_aux_density.assign(b_aux_density ? b_aux_density : nullptr, b_aux_density ? b_aux_density + w->b_aux_words : nullptr);
+  auto prefix = [](const std::vector<uint64_t>& d, size_t words) {
+    std::vector<size_t> pc(words + 1, 0);
+    for (size_t k = 0; k < words; k++) pc[k + 1] = pc[k] + (size_t)__builtin_popcountll(d[k]);
+    return pc;
+  };
+  w->a_aux_prefix = prefix(w->a_aux_density, w->a_aux_words);
+  w->b_aux_prefix = prefix(w->b_aux_density, w->b_aux_words);
+  w->a_aux_total = popcount_words(w->a_aux_density, na);
+  w->b_in_total = popcount_words(w->b_input_density, ni);
+  w->b_aux_total = popcount_words(w->b_aux_density, na);
+  const size_t tw = w->a_aux_words + w->b_in_words + w->b_aux_words;
+  BH_TRY_HIP(w->dens.alloc(std::max<size_t>(tw, 1) * 8));
+  return BH_OK;
+}
+
+bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                              const uint64_t* inputs, const uint64_t* aux, hipStream_t st, UploadSync* up) {
+  uint64_t* d = w->dens.as<uint64_t>();
+  if (w->a_aux_words)
+    BH_TRY_HIP(hipMemcpyAsync(d, w->a_aux_density.data(), w->a_aux_words * 8, hipMemcpyHostToDevice, st));
+  if (w->b_in_words)
+    BH_TRY_HIP(hipMemcpyAsync(d + w->a_aux_words, w->b_input_density.data(), w->b_in_words * 8,
+                              hipMemcpyHostToDevice, st));
+  if (w->b_aux_words)
+    BH_TRY_HIP(hipMemcpyAsync(d + w->a_aux_words + w->b_in_words, w->b_aux_density.data(), w->b_aux_words * 8,
+                              hipMemcpyHostToDevice, st));
+  HostPool& pool = ctx_pool(ctx);
+  const size_t ni = w->num_inputs, na = w->num_aux, nc = w->num_constraints, m = w->m;
+  if (ni) {
+    BH_TRY_HIP(ctx->ring.copy(pool, w->inputs.p, inputs, ni * 32, st));
+    BH_TRY_HIP(scalars_prepare(w->inputs.as<uint32_t>(), w->inputs.as<uint32_t>(), ni, 1, 0, st));
+  }
+  if (na) {
+    BH_TRY_HIP(ctx->ring.copy(pool, w->aux.p, aux, na * 32, st));
+    BH_TRY_HIP(scalars_prepare(w->aux.as<uint32_t>(), w->aux.as<uint32_t>(), na, 1, 0, st));
+  }
+  if (up) {
+    BH_TRY_HIP(hipEventRecord(up->ev[0], st));
+    up->set(1);
+  }
+  uint32_t* abc = w->abc.as<uint32_t>();
+  bh_status s;
+  if ((s = upload_fr_staged(ctx, a, nc, m, abc, st))) return s;
+  if ((s = upload_fr_staged(ctx, b, nc, m, abc + m * 8, st))) return s;
+  if ((s = upload_fr_staged(ctx, c, nc, m, abc + 2 * m * 8, st))) return s;
+  if (up) {
+    BH_TRY_HIP(hipEventRecord(up->ev[1], st));
+    up->set(2);
+  }
+  return BH_OK;
+}
+
+// always leaves `up` in a final stage (2, or -1 with the status) so that no waiter hangs
+bh_status witness_device(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                         const uint64_t* inputs, const uint64_t* aux, hipStream_t st, UploadSync* up) {
+  bh_status s = witness_device_impl(ctx, w, a, b, c, inputs, aux, st, up);
+  if (s && up) up->set(-1, s);
+  return s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -166,61 +253,15 @@ bh_status bh_witness_upload(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, c
                             const uint64_t* inputs, size_t ni, const uint64_t* aux, size_t na,
                             const uint64_t* a_aux_density, const uint64_t* b_input_density,
                             const uint64_t* b_aux_density, bh_witness** out) {
-  if (!ctx || !out || (nc && (!a || !b || !c)) || (ni && !inputs) || (na && !aux)) return BH_ERR_INVALID_ARGUMENT;
-  if ((na && (!a_aux_density || !b_aux_density)) || (ni && !b_input_density)) return BH_ERR_INVALID_ARGUMENT;
-  size_t m;
-  uint32_t L;
-  bh_status s = bh_domain_size(nc, &m, &L);  // EvaluationDomain::from_coeffs, prover.rs:211-213
-  if (s) return s;
+  if (!ctx || !out) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
   std::unique_ptr<bh_witness> w(new bh_witness());
-  w->ctx = ctx;
-  w->num_constraints = nc; w->m = m; w->log_m = (int)L; w->num_inputs = ni; w->num_aux = na;
-  BH_TRY_HIP(w->abc.alloc(3 * m * 32));
-  uint32_t* abc = w->abc.as<uint32_t>();
-  if ((s = upload_fr(ctx, a, nc, m, abc))) return s;
-  if ((s = upload_fr(ctx, b, nc, m, abc + m * 8))) return s;
-  if ((s = upload_fr(ctx, c, nc, m, abc + 2 * m * 8))) return s;
-  BH_TRY_HIP(w->inputs.alloc(std::max<size_t>(ni, 1) * 32));
-  BH_TRY_HIP(w->aux.alloc(std::max<size_t>(na, 1) * 32));
-  if (ni) {
-    BH_TRY_HIP(hipMemcpyAsync(w->inputs.p, inputs, ni * 32, hipMemcpyHostToDevice, ctx->stream));
-    BH_TRY_HIP(scalars_prepare(w->inputs.as<uint32_t>(), w->inputs.as<uint32_t>(), ni, 1, 0, ctx->stream));
-  }
-  if (na) {
-    BH_TRY_HIP(hipMemcpyAsync(w->aux.p, aux, na * 32, hipMemcpyHostToDevice, ctx->stream));
-    BH_TRY_HIP(scalars_prepare(w->aux.as<uint32_t>(), w->aux.as<uint32_t>(), na, 1, 0, ctx->stream));
-  }
-  w->a_aux_words = (na + 63) / 64;
-  w->b_in_words = (ni + 63) / 64;
-  w->b_aux_words = (na + 63) / 64;
-  w->a_aux_density.assign(a_aux_density ? a_aux_density : nullptr, a_aux_density ? a_aux_density + w->a_aux_words : nullptr);
-  w->b_input_density.assign(b_input_density ? b_input_density : nullptr,
-                            b_input_density ? b_input_density + w->b_in_words : nullptr);
-  w->b_aux_density.assign(b_aux_density ? b_aux_density : nullptr, b_aux_density ? b_aux_density + w->b_aux_words : nullptr);
-  auto prefix = [](const std::vector<uint64_t>& d, size_t words) {
-    std::vector<size_t> pc(words + 1, 0);
-    for (size_t k = 0; k < words; k++) pc[k + 1] = pc[k] + (size_t)__builtin_popcountll(d[k]);
-    return pc;
-  };
-  w->a_aux_prefix = prefix(w->a_aux_density, w->a_aux_words);
-  w->b_aux_prefix = prefix(w->b_aux_density, w->b_aux_words);
-  w->a_aux_total = popcount_words(w->a_aux_density, na);
-  w->b_in_total = popcount_words(w->b_input_density, ni);
-  w->b_aux_total = popcount_words(w->b_aux_density, na);
-  const size_t tw = w->a_aux_words + w->b_in_words + w->b_aux_words;
-  BH_TRY_HIP(w->dens.alloc(std::max<size_t>(tw, 1) * 8));
-  uint64_t* d = w->dens.as<uint64_t>();
-  if (w->a_aux_words)
-    BH_TRY_HIP(hipMemcpyAsync(d, w->a_aux_density.data(), w->a_aux_words * 8, hipMemcpyHostToDevice, ctx->stream));
-  if (w->b_in_words)
-    BH_TRY_HIP(hipMemcpyAsync(d + w->a_aux_words, w->b_input_density.data(), w->b_in_words * 8,
-                              hipMemcpyHostToDevice, ctx->stream));
-  if (w->b_aux_words)
-    BH_TRY_HIP(hipMemcpyAsync(d + w->a_aux_words + w->b_in_words, w->b_aux_density.data(), w->b_aux_words * 8,
-                              hipMemcpyHostToDevice, ctx->stream));
-  BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  bh_status s = witness_host(ctx, w.get(), a, b, c, nc, inputs, ni, aux, na, a_aux_density, b_input_density,
+                             b_aux_density);
+  if (s) return s;
+  if ((s = witness_device(ctx, w.get(), a, b, c, inputs, aux, ctx->h2d, nullptr))) return s;
+  BH_TRY_HIP(hipStreamSynchronize(ctx->h2d));
   *out = w.release();
   return BH_OK;
 }
@@ -306,6 +347,16 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
   srs->win_lo = lo;
   srs->win_hi = hi;
   return BH_OK;
+}
+
+// BH_ACC_EVENTS=0: no timing events around the accumulations (A/B of their cost; the
+// accumulation timings of bh_last_timings then read 0)
+bool acc_events_on() {
+  static const bool v = [] {
+    const char* e = getenv("BH_ACC_EVENTS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 // One multiexp of create_proof (prover.rs:233-307) as planned for a shard.
@@ -498,7 +549,8 @@ bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t n
 // `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
 // res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
 bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
-                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true) {
+                       Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
+                       UploadSync* up = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
   bh_params* mparams = const_cast<bh_params*>(params);
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
@@ -601,6 +653,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                         jobs)))
       return s;
   }
+  if (up) {  // witness still uploading (bh_prove): density maps, inputs and aux first
+    if (!up->wait(1)) return up->status;
+    BH_TRY_HIP(hipStreamWaitEvent(sS, up->ev[0], 0));
+  }
   if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
   if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), sS));
@@ -638,6 +694,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (hs) return hs;
       hipEventRecord(ctx->ev[1], sH);
       return BH_OK;
+    }
+    if (up) {  // a, b, c still uploading (bh_prove)
+      if (!up->wait(2)) return up->status;
+      BH_TRY_HIP(hipStreamWaitEvent(sH, up->ev[1], 0));
     }
     uint32_t* abc = ctx->staging.as<uint32_t>();
     BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
@@ -739,18 +799,26 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const size_t n = his[j] - los[j];
     BH_TRY_HIP(hipStreamWaitEvent(st, jev[16 + j], 0));
     MsmTiming tm;
-    tm.ev_acc_begin = jev[2 * j];
-    tm.ev_acc_end = jev[2 * j + 1];
+    tm.ev_acc_begin = acc_events_on() ? jev[2 * j] : nullptr;
+    tm.ev_acc_end = acc_events_on() ? jev[2 * j + 1] : nullptr;
     const uint32_t* bases = use_table[j] ? J.srs->win_global() : J.srs->pts.as<uint32_t>();
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
     return BH_OK;
   };
+  // BH_TAIL_DEFER=1: every reduction tail starts after the LAST accumulation (A/B: tails
+  // running beside the accumulations take SIMD slots from them)
+  static const bool tail_defer = [] {
+    const char* e = getenv("BH_TAIL_DEFER");
+    return e && e[0] == '1';
+  }();
+  int last_acc = -1;
   auto tail_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
     BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + j], 0));
+    if (tail_defer && last_acc >= 0) BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + last_acc], 0));
     // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
     // (copied here, off the accumulation stream)
     const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
@@ -780,8 +848,23 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   int h_pos = nbig;
   for (int q = 0; q < nbig; q++)
     if (jobs[big[q]].is_h) h_pos = q;
-  // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it (the
-  // distributed default: its RCCL all-to-alls never wait behind a whole-GPU accumulation);
+  // The last accumulated multiexp's reduction tail runs alone on an idle GPU, at the end of
+  // the critical path: give its bucket reduction more, shorter chains (fewer buckets per
+  // thread, down to one: ~22 instead of ~34 serial point operations at 2^15 buckets), while
+  // the earlier tails, which share the SIMDs with accumulations, keep the work-lean shape.
+  if (nbig > 0) {
+    MsmShape& sl = shapes[big[nbig - 1]];
+    static const int last_threads = [] {
+      const char* e = getenv("BH_LAST_TAIL_THREADS");
+      return e ? atoi(e) : 32768;
+    }();
+    if (last_threads > 0) {
+      int L = sl.L;
+      while (L > 1 && (size_t)sl.Wb * (size_t)(sl.NB / L) < (size_t)last_threads) L >>= 1;
+      sl.L = L;
+    }
+  }
+  // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it;
   // 1 = from the start, concurrent with everything; 2 = after the first accumulation (the
   // replicated default: H's ~4.5 ms of NTT work fills the later accumulations' round
   // boundaries and is done before h, accumulated last; ~1 ms faster than 1 at 2^22).
@@ -789,7 +872,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const char* e = getenv("BH_H_MODE");
     return e ? atoi(e) : -1;
   }();
-  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 0 : 2);
+  // 3 = concurrent with everything like 1, but enqueued by the host after the first
+  // accumulation (enqueueing H's passes and all-to-alls takes the host ~0.4 ms that the first
+  // sort would otherwise wait for).  Distributed default: 3 -- its all-to-alls run beside the
+  // first accumulations (h is accumulated last); 1 was -0.45 ms per rank against 0 at N = 8
+  // in the one-GPU rehearsal.
+  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 3 : 2);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -817,7 +905,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (sorder[r] == big[0] || (nbig > 1 && h_pos != 1 && sorder[r] == big[1])) pre_sorts = r + 1;
   bool h_in_pre = false;
   for (int r = 0; r < pre_sorts; r++) h_in_pre = h_in_pre || jobs[sorder[r]].is_h;
-  if (h_in_pre && h_mode == 2) h_mode = 1;  // h's own sort is among the first: H first
+  if (h_in_pre && (h_mode == 2 || h_mode == 3)) h_mode = 1;  // h's own sort is among the first: H first
   if (h_mode == 0 || h_mode == 1) {
     if ((s = enqueue_h(jev[33]))) return s;
   }
@@ -832,12 +920,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
+  if (h_mode == 3 && (s = enqueue_h(jev[33]))) return s;
   for (int r = pre_sorts; r < ns; r++) {
     if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
     if ((s = sort_job(sorder[r], sS))) return s;
   }
   for (int q = 1; q < nbig; q++)
     if ((s = acc_job(big[q], sA))) return s;
+  if (nbig > 0) last_acc = big[nbig - 1];
   if ((s = run_small())) return s;
   for (int q = 0; q < nbig; q++)
     if ((s = tail_job(big[q], tails[q]))) return s;
@@ -857,7 +947,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const Job& J = jobs[j];
     if (his[j] == los[j]) continue;
     float t = 0;
-    (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
+    if (acc_events_on()) (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
     const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
     if (J.g2) {
       res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].Wb, shapes[j].c);
@@ -998,6 +1088,22 @@ struct LocalExchanger : Exchanger {
   }
 };
 
+// Rehearsal of ONE rank of an N-rank run on one device: the all-to-alls move this rank's own
+// chunks only (the same copy volume per rank as the real exchange, minus the link), so the
+// device work and its timing are those of the rank, the data is not (the result is discarded).
+struct SelfExchanger : Exchanger {
+  int r, n;
+  SelfExchanger(int rr, int nn) : r(rr), n(nn) {}
+  int rank() const override { return r; }
+  int size() const override { return n; }
+  bh_status exchange(const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec, hipStream_t st) override {
+    for (int v = 0; v < nvec; v++)
+      BH_TRY_HIP(hipMemcpyAsync(recv + (size_t)v * M * 8, send + (size_t)v * M * 8, M * 32, hipMemcpyDeviceToDevice,
+                                st));
+    return BH_OK;
+  }
+};
+
 inline int dev_of(const bh_ctx* c) { return c ? c->device : -1; }
 // Parameters and witnesses live in one device's HBM: a context of another device cannot use them
 bool same_device(const bh_ctx* ctx, const bh_params* p, const bh_witness* w) {
@@ -1007,8 +1113,9 @@ bool same_device(const bh_ctx* ctx, const bh_params* p, const bh_witness* w) {
 // compute_msms, and on failure wait for whatever it had already enqueued on the context's
 // streams (the next call reuses the same workspaces)
 bh_status compute_msms_sync(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
-                            Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true) {
-  bh_status s = compute_msms(ctx, params, w, shard, nshards, res1, res2, ex, may_build);
+                            Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
+                            UploadSync* up = nullptr) {
+  bh_status s = compute_msms(ctx, params, w, shard, nshards, res1, res2, ex, may_build, up);
   if (s) ctx_sync_all(ctx);
   return s;
 }
@@ -1185,6 +1292,22 @@ bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, 
   return run_ranks(ctxs, ps, w, partials_out, false);
 }
 
+bh_status bh_rehearse_rank(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t rank, size_t nranks,
+                           double* ms) {
+  if (!ctx || !params || !w || nranks == 0 || rank >= nranks) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, w)) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  SelfExchanger ex((int)rank, (int)nranks);
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  const auto t0 = std::chrono::steady_clock::now();
+  bh_status s = compute_msms_sync(ctx, params, w, rank, nranks, r1, r2, &ex);
+  if (s) return s;
+  if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BH_OK;
+}
+
 bh_status bh_prove_witness_partials_ranks(bh_ctx* const* ctxs, const bh_params* const* params, const bh_witness* w,
                                           size_t nranks, uint8_t* partials_out) {
   if (!ctxs || !params || !w || !partials_out || nranks == 0 || nranks > 64) return BH_ERR_INVALID_ARGUMENT;
@@ -1261,13 +1384,40 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
                    size_t nc, const uint64_t* inputs, size_t ni, const uint64_t* aux, size_t na,
                    const uint64_t* a_aux_density, const uint64_t* b_input_density, const uint64_t* b_aux_density,
                    const uint64_t r[4], const uint64_t s[4], uint8_t proof_out[192]) {
-  bh_witness* w = nullptr;
-  bh_status st = bh_witness_upload(ctx, a, b, c, nc, inputs, ni, aux, na, a_aux_density, b_input_density,
-                                   b_aux_density, &w);
+  if (!ctx || !params || !r || !s || !proof_out) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, nullptr)) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  // the witness streams in on the copy stream while the proof is enqueued: its sorts start
+  // once aux has landed, the H block once a, b, c have (pinned ring + memcpy threads)
+  if (!ctx->dropin) ctx->dropin = new bh_witness();
+  bh_witness* w = ctx->dropin;
+  bh_status st = witness_host(ctx, w, a, b, c, nc, inputs, ni, aux, na, a_aux_density, b_input_density,
+                              b_aux_density);
   if (st) return st;
-  st = bh_prove_witness(ctx, params, w, r, s, proof_out);
-  bh_witness_free(w);
-  return st;
+  UploadSync up;
+  BH_TRY_HIP(hipEventCreateWithFlags(&up.ev[0], hipEventDisableTiming));
+  BH_TRY_HIP(hipEventCreateWithFlags(&up.ev[1], hipEventDisableTiming));
+  struct EvGuard {
+    UploadSync& u;
+    ~EvGuard() { for (auto e : u.ev) if (e) (void)hipEventDestroy(e); }
+  } evg{up};
+  bh_status ust = BH_OK;
+  std::thread uploader([&] {
+    if (hipSetDevice(ctx->device) != hipSuccess) { ust = BH_ERR_HIP; up.set(-1, ust); return; }
+    ust = witness_device(ctx, w, a, b, c, inputs, aux, ctx->h2d, &up);
+  });
+  Jac<Fp> r1[6];
+  Jac<bh::Fp2> r2[2];
+  st = compute_msms_sync(ctx, params, w, 0, 1, r1, r2, nullptr, true, &up);
+  uploader.join();
+  (void)hipStreamSynchronize(ctx->h2d);
+  if (st) return st;
+  if (ust) return ust;
+  assemble(vk_of(params), r1, r2, r, s, proof_out);
+  ctx->last_timings[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BH_OK;
 }
 
 bh_status bh_last_timings(const bh_ctx* ctx, double out[10]) {

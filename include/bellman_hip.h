@@ -193,6 +193,12 @@ bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, 
  * the processes of a multi-GPU run hold them); the witness is shared. */
 bh_status bh_prove_witness_partials_ranks(bh_ctx* const* ctxs, const bh_params* const* params, const bh_witness* w,
                                           size_t nranks, uint8_t* partials_out);
+/* Rehearsal of rank `rank` of an nranks-GPU run on this one device: exactly that rank's
+ * device work (its shards, the distributed H block when it applies) with each all-to-all
+ * moving only the rank's own chunks; *ms = host wall time of the rank's proof.  The partial
+ * sums are discarded (the data crossing ranks is missing): for timing and profiling only. */
+bh_status bh_rehearse_rank(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t rank, size_t nranks,
+                           double* ms);
 bh_status bh_ctx_synchronize(bh_ctx* ctx);
 int bh_device_count(void);
 

@@ -47,7 +47,7 @@ def test_rccl_single_rank_communicator(ctx):
 def test_ranks_with_shard_tables_equal_single_proof(ctx, logc, nranks):
     """Each rank: own context, own Parameters prepared with bh_params_prepare_shard (slices of
     l/a/b_g1/b_g2 and, for N >= 4, the gathered h share), then all ranks run concurrently
-    with device-copy all-to-alls.  At 2^18 every shard is large enough for tables."""
+    with device-copy all-to-alls.  At 2^18 / 4 ranks every shard is large enough for tables."""
     bh = _bh()
     rounds = (1 << (logc - 1)) - 1
     params = bh.Parameters.chain(ctx, rounds)
@@ -61,7 +61,7 @@ def test_ranks_with_shard_tables_equal_single_proof(ctx, logc, nranks):
         parts = bh.prove_witness_partials_ranks(ctxs, ps, w)
         assert bh.proof_from_partials(params.vk_bytes(), parts, nranks, R, S) == single
         st = ctxs[0].last_stats()
-        if logc >= 18:
+        if (1 << logc) // nranks >= 1 << 16:  # shards this large use window tables
             assert st[10] == st[11] > 0  # every large multiexp of rank 0 used its table slice
             assert st[12] > 0
         # and once more (tables resident, nothing rebuilt)
@@ -74,11 +74,11 @@ def test_ranks_with_shard_tables_equal_single_proof(ctx, logc, nranks):
 def test_shard_tables_are_a_slice(ctx):
     """A rank's tables hold ~1/N of the single-GPU table bytes (capacity 1/N)."""
     bh = _bh()
-    rounds = (1 << 17) - 1
+    rounds = (1 << 18) - 1
     w = bh.Witness.chain(ctx, rounds)
     full = bh.Parameters.chain(ctx, rounds)
     full.prepare(w, 4)
-    bh.prove_witness_partial(ctx, full, w, 0, 4)
+    bh.prove_witness_partial(ctx, full, w, 1, 4)
     full_bytes = ctx.last_stats()[12]
     shard = bh.Parameters.chain(ctx, rounds)
     shard.prepare_shard(w, 1, 4, distributed_h=False)
