@@ -123,6 +123,9 @@ def _load():
         "bh_prove_witness_partials_ranks": (I, [P, P, P, S, P]),
         "bh_chain_sizes": (I, [S, P]),
         "bh_rehearse_rank": (I, [P, P, P, S, S, P]),
+        "bh_multiexp_submit": (I, [P, P, S, P, S, P, S, I, P]),
+        "bh_multiexp_wait": (I, [P, P]),
+        "bh_prove_batch": (I, [P, P, P, S, P, P, I, P]),
         "bh_chain_assignment": (I, [S, U64, U64, P, P, P, P, P, P, P, P]),
         "bh_comm_allreduce_max": (I, [P, P]),
         "bh_comm_info": (I, [P, P]),
@@ -149,6 +152,7 @@ EXPORTED_SYMBOLS = [
     "bh_chain_witness_preimage", "bh_prove_witness_partial_comm", "bh_prove_witness_partials_local",
     "bh_comm_allgather", "bh_comm_allreduce_max", "bh_comm_info", "bh_params_prepare_shard", "bh_last_stats",
     "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
+    "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch",
 ]
 PARTIAL_BYTES = 960
 
@@ -305,6 +309,48 @@ def multiexp(ctx, bases, offset, density, exponents, montgomery=False):
                             BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, _ptr(out)),
            "bh_multiexp")
     return out.tobytes()
+
+
+class Waiter:
+    """multicore.rs:94-110: the pending result of multiexp_async; wait() returns the
+    uncompressed affine point (or raises the multiexp's SynthesisError)."""
+
+    def __init__(self, handle, group):
+        self.h, self.group = handle, group
+
+    def wait(self):
+        if self.h is None:
+            raise RuntimeError("Waiter already waited")
+        out = np.zeros(96 if self.group == BH_G1 else 192, dtype=np.uint8)
+        h, self.h = self.h, None
+        _check(_lib.bh_multiexp_wait(h, _ptr(out)), "bh_multiexp_wait")
+        return out.tobytes()
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None:
+            try:
+                _lib.bh_multiexp_wait(self.h, None)
+            except Exception:
+                pass
+
+
+def multiexp_async(ctx, bases, offset, density, exponents, montgomery=False):
+    """multiexp::multiexp returning a Waiter (bh_multiexp_submit); arguments as multiexp()."""
+    if isinstance(exponents, np.ndarray):
+        ex = np.ascontiguousarray(exponents, dtype=np.uint64).reshape(-1, 4)
+    else:
+        ex = fr_to_mont(exponents) if montgomery else fr_to_canonical_limbs(exponents)
+    n = ex.shape[0]
+    bits = None
+    if density is not None and not isinstance(density, FullDensity) and density is not FullDensity:
+        bits = density.bv if hasattr(density, "bv") else list(density)
+    dw = density_words(bits) if bits is not None else None
+    h = ctypes.c_void_p()
+    _check(_lib.bh_multiexp_submit(ctx.h, bases.h, offset, _ptr(dw), len(bits) if bits is not None else 0,
+                                   _ptr(ex) if n else None, n,
+                                   BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, ctypes.byref(h)),
+           "bh_multiexp_submit")
+    return Waiter(h, bases.group)
 
 
 # ------------------------------------------------------------------ EvaluationDomain
@@ -618,6 +664,17 @@ def prove(ctx, params, asg, r, s):
                          A[3].shape[0], _ptr(A[4]), A[4].shape[0], _ptr(D[0]), _ptr(D[1]), _ptr(D[2]), _ptr(rr),
                          _ptr(ss), _ptr(out)), "bh_prove")
     return out.tobytes()
+
+
+def prove_batch(ctx, params, witnesses, r, s, lanes=0):
+    """Throughput mode: len(witnesses) independent proofs pipelined on one device
+    (bh_prove_batch) -> list of Proof::write bytes."""
+    k = len(witnesses)
+    wa = (ctypes.c_void_p * max(k, 1))(*[w.h.value for w in witnesses])
+    out = np.zeros(max(k, 1) * 192, dtype=np.uint8)
+    rr, ss = fr_to_canonical_limbs([r])[0], fr_to_canonical_limbs([s])[0]
+    _check(_lib.bh_prove_batch(ctx.h, params.h, wa, k, _ptr(rr), _ptr(ss), lanes, _ptr(out)), "bh_prove_batch")
+    return [out[192 * i:192 * (i + 1)].tobytes() for i in range(k)]
 
 
 def create_proof(ctx, circuit, params, r, s):

@@ -467,6 +467,8 @@ bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, 
   }
   return BH_OK;
 }
+FrConst fr_to_dev_const() { return conv_const(FrConv::TO_DEV); }
+
 HostPool& ctx_pool(bh_ctx* ctx) {
   if (!ctx->pool) {
     // memcpy workers for the staging ring: enough to outrun PCIe, few enough for a shared box
@@ -633,8 +635,11 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (!ctx) return BH_OK;
   for (bh_ctx* v : ctx->vranks) bh_ctx_destroy(v);
   ctx->vranks.clear();
+  for (bh_ctx* v : ctx->lanes) bh_ctx_destroy(v);
+  ctx->lanes.clear();
   (void)hipSetDevice(ctx->device);
   ctx_sync_all(ctx);  // nothing may still read the workspaces released below
+  bh_ctx_release_jobs(ctx);
   if (ctx->h2d) (void)hipStreamSynchronize(ctx->h2d);
   ctx->ring.release();
   ctx->pool.reset();

@@ -67,6 +67,8 @@ struct bh_ctx_impl;
 struct DistH;
 }  // namespace bh
 
+struct bh_job_slot;  // jobs.hip: one in-flight async multiexp's stream, workspace and buffers
+
 struct bh_srs {
   bh_ctx* ctx = nullptr;
   int group = BH_G1;
@@ -118,6 +120,9 @@ struct bh_witness {
   size_t a_aux_total = 0, b_in_total = 0, b_aux_total = 0;
   // set bits before word k of each density map (k = 0..words): base index of a scalar shard
   std::vector<size_t> a_aux_prefix, b_aux_prefix;
+  // raw = true: abc/inputs/aux hold the caller's bls12_381 Montgomery words, not yet converted
+  // (bh_prove's asynchronous upload; the prover converts on its own streams)
+  bool raw = false;
 };
 
 struct bh_ctx {
@@ -154,14 +159,21 @@ struct bh_ctx {
                                     // [16,32) its continuation span (max_span)
   bh::DevBuf dspan;                 // device words for max_span
   std::vector<bh_ctx*> vranks;      // bh_prove_witness_partials_local: the virtual ranks' contexts
+  std::vector<bh_ctx*> lanes;       // bh_prove_batch: the lanes' contexts
   // host -> device staging of caller buffers (bh_prove, bh_witness_upload): H2D copy stream,
   // pinned ring, memcpy threads; dropin = the device witness bh_prove reuses call after call
   hipStream_t h2d = nullptr;
   bh::H2DRing ring;
   std::unique_ptr<bh::HostPool> pool;
   bh_witness* dropin = nullptr;
+  // bh_multiexp_submit / _wait (jobs.hip): recycled per-job resources, their own lock (a
+  // submit never waits behind a proof holding mu)
+  std::mutex jobs_mu;
+  std::vector<bh_job_slot*> all_slots, free_slots;
   std::mutex mu;
 };
+
+void bh_ctx_release_jobs(bh_ctx* ctx);
 
 namespace bh {
 bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out);
@@ -183,6 +195,8 @@ bh_status upload_fr(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, 
 // the same through the context's pinned staging ring, enqueued on st (caller holds ctx->mu)
 bh_status upload_fr_staged(bh_ctx* ctx, const uint64_t* host, size_t n, size_t padded, uint32_t* dst, hipStream_t st);
 bh::HostPool& ctx_pool(bh_ctx* ctx);
+// bls12_381 Montgomery (R = 2^256) -> device Montgomery (R = 2^261) multiplier for launch_fr_convert
+FrConst fr_to_dev_const();
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
 bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,

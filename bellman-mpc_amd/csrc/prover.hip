@@ -148,6 +148,25 @@ bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, con
                               hipMemcpyHostToDevice, st));
   HostPool& pool = ctx_pool(ctx);
   const size_t ni = w->num_inputs, na = w->num_aux, nc = w->num_constraints, m = w->m;
+  uint32_t* abc = w->abc.as<uint32_t>();
+  if (up) {
+    // asynchronous (bh_prove): DMA only -- a conversion kernel on this stream would wait for
+    // CUs behind the running accumulations and stall the copies queued after it; the
+    // prover's own streams convert (compute_msms: aux/inputs before the sorts, a/b/c into
+    // the H block's buffer)
+    w->raw = true;
+    if (ni) BH_TRY_HIP(ctx->ring.copy(pool, w->inputs.p, inputs, ni * 32, st));
+    if (na) BH_TRY_HIP(ctx->ring.copy(pool, w->aux.p, aux, na * 32, st));
+    BH_TRY_HIP(hipEventRecord(up->ev[0], st));
+    up->set(1);
+    const uint64_t* src[3] = {a, b, c};
+    for (int v = 0; v < 3; v++)
+      if (nc) BH_TRY_HIP(ctx->ring.copy(pool, abc + (size_t)v * m * 8, src[v], nc * 32, st));
+    BH_TRY_HIP(hipEventRecord(up->ev[1], st));
+    up->set(2);
+    return BH_OK;
+  }
+  w->raw = false;
   if (ni) {
     BH_TRY_HIP(ctx->ring.copy(pool, w->inputs.p, inputs, ni * 32, st));
     BH_TRY_HIP(scalars_prepare(w->inputs.as<uint32_t>(), w->inputs.as<uint32_t>(), ni, 1, 0, st));
@@ -156,19 +175,10 @@ bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, con
     BH_TRY_HIP(ctx->ring.copy(pool, w->aux.p, aux, na * 32, st));
     BH_TRY_HIP(scalars_prepare(w->aux.as<uint32_t>(), w->aux.as<uint32_t>(), na, 1, 0, st));
   }
-  if (up) {
-    BH_TRY_HIP(hipEventRecord(up->ev[0], st));
-    up->set(1);
-  }
-  uint32_t* abc = w->abc.as<uint32_t>();
   bh_status s;
   if ((s = upload_fr_staged(ctx, a, nc, m, abc, st))) return s;
   if ((s = upload_fr_staged(ctx, b, nc, m, abc + m * 8, st))) return s;
   if ((s = upload_fr_staged(ctx, c, nc, m, abc + 2 * m * 8, st))) return s;
-  if (up) {
-    BH_TRY_HIP(hipEventRecord(up->ev[1], st));
-    up->set(2);
-  }
   return BH_OK;
 }
 
@@ -656,6 +666,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (up) {  // witness still uploading (bh_prove): density maps, inputs and aux first
     if (!up->wait(1)) return up->status;
     BH_TRY_HIP(hipStreamWaitEvent(sS, up->ev[0], 0));
+    if (w->raw) {  // bls12_381 Montgomery -> canonical scalars, here rather than on the copy stream
+      uint32_t* in = const_cast<uint32_t*>(w->inputs.as<uint32_t>());
+      uint32_t* ax = const_cast<uint32_t*>(w->aux.as<uint32_t>());
+      if (ni) BH_TRY_HIP(scalars_prepare(in, in, ni, 1, 0, sS));
+      if (na) BH_TRY_HIP(scalars_prepare(ax, ax, na, 1, 0, sS));
+    }
   }
   if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
@@ -695,12 +711,22 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       hipEventRecord(ctx->ev[1], sH);
       return BH_OK;
     }
+    uint32_t* abc = ctx->staging.as<uint32_t>();
     if (up) {  // a, b, c still uploading (bh_prove)
       if (!up->wait(2)) return up->status;
       BH_TRY_HIP(hipStreamWaitEvent(sH, up->ev[1], 0));
     }
-    uint32_t* abc = ctx->staging.as<uint32_t>();
-    BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
+    if (w->raw) {  // convert into the H block's buffer (bls12_381 -> device Montgomery), zero padding
+      const size_t nc = w->num_constraints;
+      for (int v = 0; v < 3; v++) {
+        if (nc) launch_fr_convert(w->abc.as<uint32_t>() + (size_t)v * m * 8, abc + (size_t)v * m * 8, nc,
+                                  fr_to_dev_const(), 0, sH);
+        if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
+      }
+      BH_TRY_HIP(hipGetLastError());
+    } else {
+      BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
+    }
     bh_status hs = run_h_pipeline(ctx, D, abc, sH);
     if (hs) return hs;
     // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
@@ -1305,6 +1331,66 @@ bh_status bh_rehearse_rank(bh_ctx* ctx, const bh_params* params, const bh_witnes
   bh_status s = compute_msms_sync(ctx, params, w, rank, nranks, r1, r2, &ex);
   if (s) return s;
   if (ms) *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return BH_OK;
+}
+
+bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
+                         const uint64_t r_in[4], const uint64_t s_in[4], int lanes, uint8_t* proofs_out) {
+  if (!ctx || !params || !ws || !r_in || !s_in || !proofs_out || lanes < 0 || lanes > 16) return BH_ERR_INVALID_ARGUMENT;
+  if (!same_device(ctx, params, nullptr)) return BH_ERR_INVALID_ARGUMENT;
+  for (size_t i = 0; i < k; i++)
+    if (!ws[i] || !same_device(ctx, nullptr, ws[i])) return BH_ERR_INVALID_ARGUMENT;
+  if (k == 0) return BH_OK;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  // Throughput mode (BASELINE.json configs[4]): independent proofs (r, s fixed, prover.rs:158-173)
+  // on `lanes` contexts of this device, each driven by a host thread through a share of the
+  // batch, so one proof's start-up (sorts, H) and reduction tails fill the bubbles of
+  // another's accumulations; proofs_out[i] is exactly bh_prove_witness(ws[i]).
+  const int L = (int)std::min<size_t>(lanes ? (size_t)lanes : 2, k);
+  while ((int)ctx->lanes.size() < L) {
+    bh_ctx* v = nullptr;
+    bh_status st = bh_ctx_create(ctx->device, &v);
+    if (st) return st;
+    ctx->lanes.push_back(v);
+  }
+  for (int l = 0; l < L; l++) {
+    ctx->lanes[l]->tables = ctx->tables;
+    ctx->lanes[l]->window_override = ctx->window_override;
+  }
+  {  // every table the batch needs, built once before the lanes start (they never build)
+    std::unique_lock<std::shared_mutex> pwr(const_cast<bh_params*>(params)->mu);
+    for (size_t i = 0; i < k; i++) {
+      bool seen = false;
+      for (size_t j = 0; j < i && !seen; j++)
+        seen = ws[j]->m == ws[i]->m && ws[j]->num_aux == ws[i]->num_aux && ws[j]->a_aux_total == ws[i]->a_aux_total &&
+               ws[j]->b_aux_total == ws[i]->b_aux_total;
+      if (seen) continue;
+      Job jobs[8];
+      bh_status st = plan_shard(ctx->lanes[0], params, ws[i], 0, 1, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                nullptr, true, jobs);
+      if (st) return st;
+    }
+  }
+  const VkHost vk = vk_of(params);
+  std::vector<bh_status> st(L, BH_OK);
+  std::vector<std::thread> th;
+  for (int l = 0; l < L; l++)
+    th.emplace_back([&, l] {
+      bh_ctx* v = ctx->lanes[l];
+      std::lock_guard<std::mutex> vl(v->mu);
+      if (hipSetDevice(v->device) != hipSuccess) { st[l] = BH_ERR_HIP; return; }
+      for (size_t i = (size_t)l; i < k; i += (size_t)L) {
+        Jac<Fp> r1[6];
+        Jac<bh::Fp2> r2[2];
+        st[l] = compute_msms_sync(v, params, ws[i], 0, 1, r1, r2, nullptr, false);
+        if (st[l]) return;
+        assemble(vk, r1, r2, r_in, s_in, proofs_out + 192 * i);
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int l = 0; l < L; l++)
+    if (st[l]) return st[l];
   return BH_OK;
 }
 

@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--cpu-1t-log-constraints", type=int, default=12, help="1-thread CPU sample (0: skip)")
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
     ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
+    ap.add_argument("--c5", type=int, default=64,
+                    help="throughput mode (BASELINE configs[4]): this many 2^20-constraint proofs split over the GPUs "
+                         "(0: skip)")
+    ap.add_argument("--c5-log-constraints", type=int, default=20)
+    ap.add_argument("--c5-lanes", type=int, default=0, help="bh_prove_batch lanes per GPU (0: library default)")
     ap.add_argument("--dropin", type=int, default=1,
                     help="also time bh_prove from host buffers (the drop-in path; 1-GPU runs)")
     return ap.parse_args()
@@ -95,6 +100,41 @@ def cpu_baseline(bh, ctx, log_c, log_c_1t):
                              "sample": f"median of 3, 2^{log_c_1t}-constraint chain, 1 thread",
                              "proof_matches_gpu": proof1 == g1}
     return out
+
+
+def c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier):
+    """BASELINE.json configs[4]: a batch of independent proofs of one circuit (distinct
+    witnesses: preimage seed 8 + i, shared Parameters), split over the ranks with no
+    collective (replicas), each rank pipelining its share with bh_prove_batch.  Returns the
+    whole-job constraints/s (max over ranks of the batch time)."""
+    from concurrent.futures import ThreadPoolExecutor
+    rounds = (1 << (args.c5_log_constraints - 1)) - 1
+    n_c = 2 * rounds + 2
+    params = bh.Parameters.chain(ctx, rounds)
+    mine = list(range(rank, args.c5, world))
+    t0 = time.time()
+    with ThreadPoolExecutor(8) as ex:  # host synthesis in parallel (ctypes releases the GIL)
+        ws = list(ex.map(lambda i: bh.Witness.chain(ctx, rounds, seed=7, preimage_seed=8 + i), mine))
+    t_syn = time.time() - t0
+    params.prepare(ws[0])
+    bh.prove_batch(ctx, params, ws[:4], r, s, args.c5_lanes)  # warm-up
+    barrier()
+    t0 = time.perf_counter()
+    proofs = bh.prove_batch(ctx, params, ws, r, s, args.c5_lanes)
+    barrier()
+    el = time.perf_counter() - t0
+    # every batched proof is the single-proof path's proof (spot-check first and last)
+    ok = (proofs[0] == bh.prove_witness(ctx, params, ws[0], r, s)
+          and proofs[-1] == bh.prove_witness(ctx, params, ws[-1], r, s) and len(set(proofs)) == len(proofs))
+    if comm is not None:
+        el = comm.allreduce_max(el)
+        ok = comm.allreduce_max(0.0 if ok else 1.0) == 0.0
+    del ws, params
+    return {"workload": f"C5: {args.c5} independent proofs of a 2^{args.c5_log_constraints}-constraint MiMC chain "
+                        f"(distinct preimages), {len(mine)} per GPU, bh_prove_batch",
+            "value": round(args.c5 * n_c / el, 1), "unit": "constraints/s", "proofs": args.c5,
+            "ms_per_proof": round(el * 1e3 / max(1, len(mine)), 3), "batch_s": round(el, 3),
+            "lanes": args.c5_lanes or 2, "proofs_match_single": ok, "synthesis_s": round(t_syn, 2)}
 
 
 def main():
@@ -196,9 +236,6 @@ def main():
         per_rank_ms = [round(json.loads(x.decode().strip()), 3)
                        for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(32))]
         elapsed = comm.allreduce_max(elapsed)
-    if rank != 0:
-        comm.close()
-        return
     ms = elapsed * 1000.0 / args.steps
     value = n_constraints * args.steps / elapsed
     # dominant kernel: G1 bucket accumulation (k_accumulate_pf<G1>), device events around every
@@ -231,6 +268,10 @@ def main():
             "mad_u64_tps": round(madd_rate * MADS_PER_G1_MADD / 1e3, 2) if madd_rate else None,
             "mad_u64_frac": round(madd_rate * MADS_PER_G1_MADD / 1e3 / MAD_U64_PEAK_TPS, 4) if madd_rate else None,
             "mad_u64_peak_tps": MAD_U64_PEAK_TPS, "mad_u64_peak_source": "tools/microbench/madbench.hip"}
+    c5 = c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier) if args.c5 else None
+    if rank != 0:
+        comm.close()
+        return
     # the drop-in path: bh_prove from the ProvingAssignment's host
     # buffers, i.e. the resident-witness step plus streaming ~0.5 GB of witness over PCIe
     # (pinned ring, overlapped with the first sorts and accumulation)
@@ -271,6 +312,7 @@ def main():
         "rccl": rccl,
         "per_rank_ms_per_step": per_rank_ms,
         "dropin": dropin,
+        "c5": c5,
         "roofline": roof,
         "valu_roofline": valu,
         "end_to_end": {"value": round(n_constraints / (t_wit + ms / 1e3), 1), "unit": "constraints/s",

@@ -98,6 +98,19 @@ bh_status bh_srs_get(const bh_srs* srs, size_t i, uint8_t* out);
 bh_status bh_multiexp(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint64_t* density_words,
                       size_t density_len, const uint64_t* exponents, size_t n, int scalar_format, uint8_t* out);
 
+/* ---- asynchronous multiexp: multiexp::multiexp returns a Waiter (multiexp.rs:252-281,
+ * multicore.rs:94-110) and create_proof keeps eight in flight (prover.rs:233-307).  submit
+ * enqueues the multiexp on a stream and workspace of its own and returns without waiting for
+ * the device (the exponents and density words are read before it returns); wait blocks on
+ * the job's event, writes the result like bh_multiexp and frees the job.  EOF / identity
+ * errors of the Source are reported by wait, as the reference reports them from wait().
+ * Thread-safe: any number of jobs per context, submitted and waited from any threads. */
+typedef struct bh_job bh_job;
+bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint64_t* density_words,
+                             size_t density_len, const uint64_t* exponents, size_t n, int scalar_format,
+                             bh_job** out);
+bh_status bh_multiexp_wait(bh_job* job, uint8_t* out);
+
 /* ---- EvaluationDomain.  Arrays hold 2^log_m Montgomery Fr (4 u64 each), in place. */
 bh_status bh_domain_size(size_t len, size_t* m, uint32_t* log_m);
 bh_status bh_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
@@ -145,6 +158,14 @@ bh_status bh_params_prepare_shard(bh_ctx* ctx, bh_params* params, const bh_witne
                                   int distributed_h);
 bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witness* w, const uint64_t r[4],
                            const uint64_t s[4], uint8_t proof_out[192]);
+
+/* Throughput mode (BASELINE.json configs[4], "C5"): k independent proofs of witnesses sharing
+ * one Parameters, pipelined on `lanes` streams-and-workspace sets of this device (0 = default,
+ * 2) so that one proof's sorts, H block and reduction tails fill the gaps of another's
+ * accumulations.  proofs_out: k * 192 bytes, proof i == bh_prove_witness(ws[i]).  Across GPUs
+ * the batch is split by the caller (one process per GPU, no collective). */
+bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
+                         const uint64_t r[4], const uint64_t s[4], int lanes, uint8_t* proofs_out);
 
 /* ---- multi-GPU: every multiexp sharded by scalar range (shard k of N covers
  * [k*n/N, (k+1)*n/N) of each query); partial_out = 8 uncompressed points

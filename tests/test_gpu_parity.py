@@ -500,3 +500,51 @@ def test_bh_prove_from_host_buffers(ctx, golden, rounds):
         assert proof.hex() == fx["proof"]
     assert proof == bh.prove_witness(ctx, params, bh.Witness.chain(ctx, rounds), 27134, 17146)
     assert bh.prove(ctx, params, asg, 27134, 17146) == proof  # buffers reused
+
+
+def test_async_multiexp_waiters_equal_sequential(ctx, golden):
+    """bh_multiexp_submit / bh_multiexp_wait (the Waiter seam, multiexp.rs:252-281 and
+    multicore.rs:94-110): eight multiexps in flight at once from one thread, as create_proof
+    keeps them (prover.rs:233-307), waited in reverse order, equal the sequential results;
+    EOF / identity errors surface from wait() like the reference's."""
+    bh = _bh()
+    rng = random.Random(99)
+    g1 = _bases(ctx, bh.BH_G1, golden["msm_g1"]["bases"])
+    g2 = _bases(ctx, bh.BH_G2, golden["msm_g2"]["bases"])
+    n1, n2 = len(golden["msm_g1"]["bases"]), len(golden["msm_g2"]["bases"])
+    jobs = []
+    for k in range(8):
+        G, bases, nb = (bh.BH_G1, g1, n1) if k % 3 else (bh.BH_G2, g2, n2)
+        n = rng.randrange(1, nb)
+        dens = [rng.random() < 0.7 for _ in range(n)] if k % 2 else None
+        exps = [rng.randrange(R) for _ in range(n)]
+        jobs.append((bases, 0, dens, exps))
+    waiters = [bh.multiexp_async(ctx, *j) for j in jobs]
+    got = [w.wait() for w in reversed(waiters)][::-1]
+    assert got == [bh.multiexp(ctx, *j) for j in jobs]
+    # error semantics from the golden cases, deferred to wait()
+    for case in golden["msm_g1"]["cases"]:
+        if "error" not in case:
+            continue
+        exps = [int(x, 16) for x in case["exps"]]
+        dens = None if case["density"] is None else [c == "1" for c in case["density"]]
+        w = bh.multiexp_async(ctx, g1, case["offset"], dens, exps)
+        with pytest.raises(bh.SynthesisError) as e:
+            w.wait()
+        assert e.value.code == case["error"]
+
+
+@pytest.mark.parametrize("logc,k,lanes", [(12, 5, 1), (12, 5, 2), (16, 6, 3), (20, 4, 2)])
+def test_prove_batch_equals_single_proofs(ctx, logc, k, lanes):
+    """Throughput mode (BASELINE.json configs[4], C5): independent proofs of distinct
+    witnesses (preimage seeds 8 + i) sharing one Parameters, pipelined on `lanes` contexts of
+    one device by bh_prove_batch, are each byte-equal to that witness's single proof (at
+    2^20 constraints, the C5 proof size, too)."""
+    bh = _bh()
+    rounds = (1 << (logc - 1)) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    ws = [bh.Witness.chain(ctx, rounds, seed=7, preimage_seed=8 + i) for i in range(k)]
+    got = bh.prove_batch(ctx, params, ws, 27134, 17146, lanes)
+    want = [bh.prove_witness(ctx, params, w, 27134, 17146) for w in ws]
+    assert got == want
+    assert len(set(got)) == k
