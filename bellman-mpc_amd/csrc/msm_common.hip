@@ -99,7 +99,27 @@ __global__ void __launch_bounds__(256) k_scalars_prepare(const uint32_t* in, uin
   const uint4* p = reinterpret_cast<const uint4*>(in + src * 8);
   uint4 a = p[0], b = p[1];
   uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  if (mode != 0) {
+  if (mode == 0) {
+    // canonical words are Scalar::to_le_bits of a field element (< r); a caller's word >= r
+    // (< 2^256 < 3r) is reduced: the reference's multiexp walks all 256 bits, and
+    // (k mod r) * P = k * P for every point of the prime-order group, so the result is the same
+    constexpr uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                               0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+    for (int it = 0; it < 2; it++) {
+      bool ge = true;
+      for (int k = 7; k >= 0; k--) {
+        if (w[k] != R[k]) { ge = w[k] > R[k]; break; }
+      }
+      if (!ge) break;
+      uint32_t borrow = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint64_t d = (uint64_t)w[k] - R[k] - borrow;
+        w[k] = (uint32_t)d;
+        borrow = (uint32_t)(d >> 63);
+      }
+    }
+  } else {
     DFr x = fe_unpack<FrCfg>(w);
     DFr k = fe_zero<FrCfg>();
     k.v[0] = (mode == 1) ? 32u : 1u;  // x*32*2^-261 = x*2^-256 ; x*2^-261

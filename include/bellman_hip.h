@@ -24,7 +24,9 @@
  *   - Fr vectors ("Montgomery") use the bls12_381 0.6 in-memory layout:
  *     4 little-endian u64 limbs of x * 2^256 mod r per element.
  *   - Exponents for bh_multiexp are Scalar::to_le_bits() words (canonical,
- *     4 LE u64 per scalar) unless BH_SCALARS_MONTGOMERY is given.
+ *     4 LE u64 per scalar) unless BH_SCALARS_MONTGOMERY is given.  A canonical word
+ *     >= r is taken mod r (the reference walks all 256 bits; k*P = (k mod r)*P in the
+ *     prime-order group, so results agree).
  *   - Density maps are bitvec<u64, Lsb0> words: bit i of word i/64 is entry i.
  *   - Group elements use the zcash/bls12_381 encodings (big-endian, flag bits
  *     in byte 0): uncompressed 96 B (G1) / 192 B (G2), compressed 48/96 B.

@@ -614,39 +614,69 @@ int bp_chain_prove(const uint8_t* params, size_t len, size_t rounds, uint64_t se
 
 int bp_hardware_threads(void) { return (int)std::thread::hardware_concurrency(); }
 
-// multiexp::multiexp over G1 with FullDensity (multiexp.rs:252-281), bellman's schedule:
-// one task per window on a pool of `threads`.  bases: n_bases uncompressed encodings;
-// exps: n canonical scalars (4 LE u64).  out: uncompressed result (0x40 flag = identity).
-// Returns 0, 1 (identity base), 2 (EOF) or 11 (bad encoding).
-int bp_multiexp_g1(const uint8_t* bases, size_t n_bases, const uint64_t* exps, size_t n, int threads,
-                   uint8_t out[96], double* ms) {
-  std::vector<Aff<Fp>> b(n_bases);
-  for (size_t i = 0; i < n_bases; i++)
-    if (!read_g1(bases + 96 * i, &b[i])) return 11;
+}  // extern "C"
+
+static void write_uncompressed(const Aff<Fp>& a, uint8_t* out) {
+  memset(out, 0, 96);
+  if (a.inf) { out[0] = 0x40; return; }
+  to_be(a.x, out);
+  to_be(a.y, out + 48);
+}
+static void write_uncompressed(const Aff<Fp2>& a, uint8_t* out) {
+  memset(out, 0, 192);
+  if (a.inf) { out[0] = 0x40; return; }
+  to_be(a.x.c1, out); to_be(a.x.c0, out + 48); to_be(a.y.c1, out + 96); to_be(a.y.c0, out + 144);
+}
+
+template <class T>
+static int multiexp_host(const uint8_t* bases, size_t n_bases, size_t offset, const uint64_t* density_words,
+                         const uint64_t* exps, size_t n, int threads, uint8_t* out, double* ms) {
+  constexpr size_t PB = sizeof(T) == sizeof(Fp) ? 96 : 192;
+  std::vector<Aff<T>> b(n_bases);
+  for (size_t i = 0; i < n_bases; i++) {
+    bool ok;
+    if constexpr (PB == 96) ok = read_g1(bases + PB * i, &b[i]);
+    else ok = read_g2(bases + PB * i, &b[i]);
+    if (!ok) return 11;
+  }
   std::vector<Fb> e(n);
   for (size_t i = 0; i < n; i++) memcpy(e[i].w, exps + 4 * i, 32);
+  std::vector<uint64_t> dens;
+  if (density_words) dens.assign(density_words, density_words + (n + 63) / 64);
   Pool pool(threads > 0 ? threads : (int)std::thread::hardware_concurrency());
   auto t0 = std::chrono::steady_clock::now();
-  MultiexpJob<Fp> job;
+  MultiexpJob<T> job;
   job.bases = &b;
-  job.offset = 0;
-  job.density = nullptr;
+  job.offset = offset;
+  job.density = density_words ? &dens : nullptr;
   job.exps = &e;
-  multiexp_spawn<Fp>(pool, &job);
+  multiexp_spawn<T>(pool, &job);
   pool.wait_all();
   if (job.err) return job.err;
-  multiexp_finish<Fp>(&job);
+  multiexp_finish<T>(&job);
   auto t1 = std::chrono::steady_clock::now();
   if (ms) *ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-  const Aff<Fp> a = to_affine(job.result);
-  memset(out, 0, 96);
-  if (a.inf) {
-    out[0] = 0x40;
-  } else {
-    to_be(a.x, out);
-    to_be(a.y, out + 48);
-  }
+  write_uncompressed(to_affine(job.result), out);
   return 0;
+}
+
+extern "C" {
+
+// multiexp::multiexp (multiexp.rs:252-281) over G1 / G2 with bellman's schedule: one task per
+// window on a pool of `threads`.  bases: n_bases uncompressed encodings (96 / 192 B);
+// base_offset: the SourceBuilder's start index; density_words: QueryDensity bit words or NULL
+// (FullDensity); exps: n canonical scalars (4 LE u64).  out: uncompressed result (0x40 flag =
+// identity).  Returns 0, 1 (identity base), 2 (EOF) or 11 (bad encoding).
+int bp_multiexp(int group, const uint8_t* bases, size_t n_bases, size_t base_offset, const uint64_t* density_words,
+                const uint64_t* exps, size_t n, int threads, uint8_t* out, double* ms) {
+  if (group == 1) return multiexp_host<Fp>(bases, n_bases, base_offset, density_words, exps, n, threads, out, ms);
+  if (group == 2) return multiexp_host<Fp2>(bases, n_bases, base_offset, density_words, exps, n, threads, out, ms);
+  return 10;
+}
+
+int bp_multiexp_g1(const uint8_t* bases, size_t n_bases, const uint64_t* exps, size_t n, int threads,
+                   uint8_t out[96], double* ms) {
+  return bp_multiexp(1, bases, n_bases, 0, nullptr, exps, n, threads, out, ms);
 }
 
 }  // extern "C"

@@ -27,6 +27,8 @@ def _lib():
     lib.bp_hardware_threads.restype = I
     lib.bp_multiexp_g1.restype = I
     lib.bp_multiexp_g1.argtypes = [P, S, P, S, I, P, P]
+    lib.bp_multiexp.restype = I
+    lib.bp_multiexp.argtypes = [I, P, S, S, P, P, S, I, P, P]
     return lib
 
 
@@ -65,4 +67,23 @@ def multiexp_g1(bases_uncompressed, exps_limbs, threads=0):
                             out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ms))
     if st:
         raise RuntimeError(f"bp_multiexp_g1 failed: {st}")
+    return out.tobytes(), ms.value
+
+
+def multiexp(group, bases_uncompressed, exps_limbs, base_offset=0, density_words=None, threads=0):
+    """bellman's multiexp over G1 (group 1) or G2 (group 2) with a base offset and an optional
+    density bitvec (uint64 words): (uncompressed bytes, ms)."""
+    lib = _lib()
+    pb = 96 if group == 1 else 192
+    b = np.frombuffer(bases_uncompressed, dtype=np.uint8)
+    e = np.ascontiguousarray(exps_limbs, dtype=np.uint64).reshape(-1, 4)
+    d = None if density_words is None else np.ascontiguousarray(density_words, dtype=np.uint64)
+    out = np.zeros(pb, dtype=np.uint8)
+    ms = ctypes.c_double()
+    st = lib.bp_multiexp(group, b.ctypes.data_as(ctypes.c_void_p), len(bases_uncompressed) // pb, base_offset,
+                         None if d is None else d.ctypes.data_as(ctypes.c_void_p),
+                         e.ctypes.data_as(ctypes.c_void_p), e.shape[0], threads,
+                         out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ms))
+    if st:
+        raise RuntimeError(f"bp_multiexp failed: {st}")
     return out.tobytes(), ms.value

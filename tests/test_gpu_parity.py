@@ -548,3 +548,89 @@ def test_prove_batch_equals_single_proofs(ctx, logc, k, lanes):
     want = [bh.prove_witness(ctx, params, w, 27134, 17146) for w in ws]
     assert got == want
     assert len(set(got)) == k
+
+
+def test_msm_canonical_exponents_at_or_above_r(ctx, golden):
+    """Exponent words >= r (k < 2^256) in the canonical format give k*P like the
+    reference's 256-bit window walk does (multiexp.rs:159-250): (k mod r)*P."""
+    bh = _bh()
+    g1 = _bases(ctx, bh.BH_G1, golden["msm_g1"]["bases"][:40])
+    rng = random.Random(5)
+    ks = [rng.randrange(R) for _ in range(40)]
+    big = [k + R if k + R < 1 << 256 else k for k in ks]
+    big[0], ks[0] = R, 0
+    big[1], ks[1] = (1 << 256) - 1, ((1 << 256) - 1) % R
+    raw = np.array([[(k >> (64 * i)) & (2**64 - 1) for i in range(4)] for k in big], dtype=np.uint64)
+    assert bh.multiexp(ctx, g1, 0, None, raw) == bh.multiexp(ctx, g1, 0, None, ks)
+
+
+def test_c1_mimc322_device_params_and_proof(ctx):
+    """C1 (BASELINE.json configs[0], mimc_mod.rs:6 MIMC_ROUNDS = 322, 646 constraints): the
+    device CRS generator reproduces the oracle's Parameters bytes, and both the resident-
+    witness prover and the drop-in bh_prove reproduce the oracle's proof; the proof verifies
+    under the oracle's pairing restatement."""
+    import hashlib
+    import json
+    import os
+    from oracle import pairing as pr
+    bh = _bh()
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, "golden", "mimc322.json")) as f:
+        fx = json.load(f)
+    params = bh.Parameters.chain(ctx, fx["rounds"])
+    pbytes = params.write()
+    assert hashlib.sha256(pbytes).hexdigest() == fx["params_sha256"]
+    proof = bh.prove_witness(ctx, params, bh.Witness.chain(ctx, fx["rounds"]), fx["r"], fx["s"])
+    assert proof.hex() == fx["proof"]
+    assert bh.prove(ctx, params, bh.chain_assignment(fx["rounds"]), fx["r"], fx["s"]).hex() == fx["proof"]
+    vk = pr.vk_from_params_bytes(params.vk_bytes())
+    assert pr.verify_proof(vk, pr.proof_from_bytes(proof), [int(fx["image"], 16)])
+
+
+@pytest.mark.parametrize("logc,tables", [(16, True), (16, False), (18, True), (18, False)])
+def test_c3_family_proof_equals_cpu_port(ctx, logc, tables):
+    """Oracle-backed parity at size: the device proof of a 2^16 / 2^18-constraint MiMC chain,
+    with and without the SRS window tables, equals the proof of the C++ restatement of
+    bellman's multicore prover (oracle/cpu) on the same Parameters bytes."""
+    from oracle import cpu_port
+    bh = _bh()
+    rounds = (1 << (logc - 1)) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    ctx.set_tables(tables)
+    try:
+        if tables:
+            params.prepare(w)
+        dev = bh.prove_witness(ctx, params, w, 27134, 17146)
+    finally:
+        ctx.set_tables(True)
+    port, _, _ = cpu_port.chain_prove(params.write(), rounds, threads=16)
+    assert dev == port
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_g2_msm_2p16_equals_cpu_port(ctx, dense):
+    """A 2^16-scalar G2 multiexp (the b_g2 query of a 2^17-constraint chain's Parameters as
+    bases, random dense scalars, optionally a density map with a base offset) equals
+    bellman's multiexp algorithm in the C++ port."""
+    from oracle import cpu_port
+    from params_bytes import split_params
+    bh = _bh()
+    params = bh.Parameters.chain(ctx, (1 << 16) - 1)
+    b_g2 = split_params(params.write())["b_g2"]
+    nb = len(b_g2) // 192
+    rng = np.random.default_rng(11)
+    n = 1 << 16
+    ex = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64)
+    ex[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)  # < 2^252 < r: canonical
+    bases = bh.Bases(ctx, bh.BH_G2, b_g2)
+    if dense:
+        off, bits = 0, None
+        ex = ex[:nb]
+    else:
+        off = 3
+        bits = rng.random(n) < (nb - off) / n * 0.98
+    words = None if bits is None else bh.density_words(list(bits))
+    got = bh.multiexp(ctx, bases, off, None if bits is None else list(bits), ex)
+    want, _ = cpu_port.multiexp(2, b_g2, ex, off, words, threads=16)
+    assert got == want
