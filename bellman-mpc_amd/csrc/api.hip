@@ -255,27 +255,43 @@ static inline Fp fp_from_dev_limbs(const uint32_t* limbs14) {
   return fp_from_dev_words(words);
 }
 
-Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, int W, int c) {
+static Jac<Fp> g1_from_xyzz(const XYZZ<FpOps>& p) {
+  return xyzz_to_jac(fp_from_dev_limbs(p.X.v), fp_from_dev_limbs(p.Y.v), fp_from_dev_limbs(p.ZZ.v),
+                     fp_from_dev_limbs(p.ZZZ.v));
+}
+// window sums -> the multiexp (Horner over the Wb windows, c doublings each; multiexp.rs:244-249),
+// or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction)
+Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, const MsmShape& sh) {
+  const int shift = reduce_split_shift(sh, false);
+  if (shift >= 0) {
+    Jac<Fp> z = g1_from_xyzz(ws[1]);
+    for (int k = 0; k < shift; k++) z = jac_dbl(z);
+    return jac_add(g1_from_xyzz(ws[0]), z);
+  }
   Jac<Fp> acc = jac_identity<Fp>();
-  for (int w = W - 1; w >= 0; w--) {
-    for (int k = 0; k < c; k++) acc = jac_dbl(acc);
-    const XYZZ<FpOps>& p = ws[w];
-    Jac<Fp> q = xyzz_to_jac(fp_from_dev_limbs(p.X.v), fp_from_dev_limbs(p.Y.v), fp_from_dev_limbs(p.ZZ.v),
-                            fp_from_dev_limbs(p.ZZZ.v));
-    acc = jac_add(acc, q);
+  for (int w = sh.Wb - 1; w >= 0; w--) {
+    for (int k = 0; k < sh.c; k++) acc = jac_dbl(acc);
+    acc = jac_add(acc, g1_from_xyzz(ws[w]));
   }
   return acc;
 }
 static inline bh::Fp2 fp2_from_dev(const DFp2& v) {
   return bh::Fp2{fp_from_dev_limbs(v.c0.v), fp_from_dev_limbs(v.c1.v)};
 }
-Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, int W, int c) {
+static Jac<bh::Fp2> g2_from_xyzz(const XYZZ<Fp2Ops>& p) {
+  return xyzz_to_jac(fp2_from_dev(p.X), fp2_from_dev(p.Y), fp2_from_dev(p.ZZ), fp2_from_dev(p.ZZZ));
+}
+Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh) {
+  const int shift = reduce_split_shift(sh, true);
+  if (shift >= 0) {
+    Jac<bh::Fp2> z = g2_from_xyzz(ws[1]);
+    for (int k = 0; k < shift; k++) z = jac_dbl(z);
+    return jac_add(g2_from_xyzz(ws[0]), z);
+  }
   Jac<bh::Fp2> acc = jac_identity<bh::Fp2>();
-  for (int w = W - 1; w >= 0; w--) {
-    for (int k = 0; k < c; k++) acc = jac_dbl(acc);
-    const XYZZ<Fp2Ops>& p = ws[w];
-    Jac<bh::Fp2> q = xyzz_to_jac(fp2_from_dev(p.X), fp2_from_dev(p.Y), fp2_from_dev(p.ZZ), fp2_from_dev(p.ZZZ));
-    acc = jac_add(acc, q);
+  for (int w = sh.Wb - 1; w >= 0; w--) {
+    for (int k = 0; k < sh.c; k++) acc = jac_dbl(acc);
+    acc = jac_add(acc, g2_from_xyzz(ws[w]));
   }
   return acc;
 }
@@ -293,7 +309,7 @@ bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, co
                                     (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
-  *out = combine_g1(ctx->g1ws.host_window_sums, sh.Wb, sh.c);
+  *out = combine_g1(ctx->g1ws.host_window_sums, sh);
   return BH_OK;
 }
 bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
@@ -307,7 +323,7 @@ bh_status msm_g2_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, co
                                     (uint32_t)base_offset, sh, acc_ms ? &tm : nullptr));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   if (acc_ms) { float t = 0; if (hipEventElapsedTime(&t, tm.ev_acc_begin, tm.ev_acc_end) == hipSuccess) *acc_ms += t; }
-  *out = combine_g2(ctx->g2ws.host_window_sums, sh.Wb, sh.c);
+  *out = combine_g2(ctx->g2ws.host_window_sums, sh);
   return BH_OK;
 }
 
@@ -434,6 +450,9 @@ bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
     const size_t n = (size_t)1 << tl;
     BH_TRY_HIP(tab.alloc(n * 9 * 4));
     launch_expand_table(tab.as<uint32_t>(), n, lo.as<uint32_t>(), hi.as<uint32_t>(), tb, ctx->stream);
+    DevBuf& lv = dir == 0 ? d->lv_fwd : d->lv_inv;
+    BH_TRY_HIP(lv.alloc(std::max<size_t>(m, 2) * 32));
+    launch_level_table(lv.as<uint32_t>(), L, tab.as<uint32_t>(), ctx->stream);
     BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   }
   d->lo_bits = (L + 1) / 2;
@@ -506,7 +525,7 @@ static bh_status run_fft(bh_ctx* ctx, Domain* D, FftKind kind, uint32_t* d_a, ui
   const uint32_t* pre_hi = nullptr;
   if (kind == COSET_FFT) { pre_lo = D->gpow_lo.as<uint32_t>(); pre_hi = D->gpow_hi.as<uint32_t>(); }
   launch_permute(d_a, d_tmp, L, pre_lo, pre_hi, D->lo_bits, ctx->stream);
-  const uint32_t* tw = (kind == FFT || kind == COSET_FFT) ? D->tw_fwd.as<uint32_t>() : D->tw_inv.as<uint32_t>();
+  const uint32_t* tw = (kind == FFT || kind == COSET_FFT) ? D->lv_fwd.as<uint32_t>() : D->lv_inv.as<uint32_t>();
   const uint32_t* post_lo = nullptr;
   const uint32_t* post_hi = nullptr;
   int post_bits = D->lo_bits;
@@ -532,26 +551,43 @@ static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind
   return download_fr(ctx, ctx->staging.as<uint32_t>(), m, coeffs);
 }
 
-// H pipeline on device-resident a|b|c (3*m packed device form, natural order). On return
-// d_abc's first m entries hold h coefficients in BIT-REVERSED order (device form).
-bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st) {
+// H pipeline (prover.rs:210-231) on device-resident a|b|c (3*m packed device form, natural
+// order) in d_abc; with src_abc the first passes read the inputs from there (the witness stays
+// untouched, no copy).  Without hout, on return d_abc's first m entries hold the h coefficients
+// in BIT-REVERSED order (device form); with hout, the last pass writes the m-1 canonical h
+// scalars in natural order to hout instead (truncation + to_le_bits fused).
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc,
+                         uint32_t* hout) {
   const int L = D->L;
   const size_t m = (size_t)1 << L;
   uint32_t* a = d_abc;
   uint32_t* b = d_abc + m * 8;
   uint32_t* c = d_abc + 2 * m * 8;
   // prover.rs:214-219: ifft (DIF, omega^-1) with m^-1 * g^i fused = ifft + distribute_powers(g);
-  // then fft (DIT, bit-reversed -> natural) = coset_fft
-  for (uint32_t* x : {a, b, c}) {
-    launch_ntt(x, L, true, D->tw_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
-               D->lo_bits, st);
-    launch_ntt(x, L, false, D->tw_fwd.as<uint32_t>(), nullptr, nullptr, 0, st);
+  // then fft (DIT, bit-reversed -> natural) = coset_fft; c's storing pass computes
+  // (a*b - c) / Z(g) into a (prover.rs:221-225: mul_assign, sub_assign, divide_by_z_on_coset)
+  for (int v = 0; v < 3; v++) {
+    uint32_t* x = d_abc + (size_t)v * m * 8;
+    launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
+               D->lo_bits, st, src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
+    NttEpilogue e;
+    if (v == 2) {
+      e.kind = NttEpilogue::AB_MINUS_C;
+      e.pa = a;
+      e.pb = b;
+      e.k = D->consts.as<uint32_t>() + 9;
+    }
+    launch_ntt(x, L, false, D->lv_fwd.as<uint32_t>(), nullptr, nullptr, 0, st, nullptr, e);
   }
-  // prover.rs:221-225: a*b - c, divide_by_z_on_coset
-  launch_pointwise(a, b, c, m, 2, D->consts.as<uint32_t>() + 9, st);
   // prover.rs:226: icoset_fft = ifft + distribute_powers(g^-1), fused as above (output bit-reversed)
-  launch_ntt(a, L, true, D->tw_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
-             D->lo_bits, st);
+  NttEpilogue e;
+  if (hout) {
+    e.kind = NttEpilogue::SCALARS;
+    e.out = hout;
+    e.n_out = (uint32_t)(m - 1);
+  }
+  launch_ntt(a, L, true, D->lv_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
+             D->lo_bits, st, nullptr, e);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
 }

@@ -55,6 +55,7 @@ struct DevBuf {
 struct Domain {
   int L = -1;
   DevBuf tw_fwd, tw_inv;                  // omega^j, omega^-j, j < m/2
+  DevBuf lv_fwd, lv_inv;                  // per-level packed twiddles (launch_level_table)
   DevBuf coset_lo, coset_hi;              // g^i split tables, hi folded with m^-1   (ifft -> coset)
   DevBuf icoset_lo, icoset_hi;            // g^-i split, hi folded with m^-1        (icoset)
   DevBuf gpow_lo, gpow_hi;                // g^i (no m^-1)                           (coset_fft input)
@@ -184,8 +185,8 @@ void fr_to_dev_limbs(const Fr& x, uint32_t out[9]);
 void fr_to_dev_packed(const Fr& x, uint32_t out[8]);
 Fr fr_from_dev_packed(const uint32_t in[8]);
 // combine per-window sums (host Horner, multiexp.rs:244-249)
-Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, int W, int c);
-Jac<Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, int W, int c);
+Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, const MsmShape& sh);
+Jac<Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh);
 // run one MSM whose scalars/index map are already on the device; returns result on host
 bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,
                         const int32_t* d_idx, Jac<Fp>* out, float* acc_ms);
@@ -198,7 +199,8 @@ bh::HostPool& ctx_pool(bh_ctx* ctx);
 // bls12_381 Montgomery (R = 2^256) -> device Montgomery (R = 2^261) multiplier for launch_fr_convert
 FrConst fr_to_dev_const();
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
-bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st);
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc = nullptr,
+                         uint32_t* hout = nullptr);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,
                          bh_srs* out);
 // reference-exact error semantics of multiexp (EOF / identity), host side

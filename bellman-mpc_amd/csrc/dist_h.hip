@@ -204,7 +204,7 @@ bh_status dist_h_phase1(bh_ctx* ctx, DistH& d, const uint32_t* abc_full, hipStre
                      (uint32_t)d.M, d.Lm, (uint32_t)d.N, (uint32_t)d.rank, 3u, m);
   // Y_r = iNTT_M of the residue class: DIT (bit-reversed in, natural out), omega_M^-1
   for (int v = 0; v < 3; v++)
-    launch_ntt(d.work.as<uint32_t>() + v * d.M * 8, d.Lm, false, Dm->tw_inv.as<uint32_t>(), nullptr, nullptr, 0, st);
+    launch_ntt(d.work.as<uint32_t>() + v * d.M * 8, d.Lm, false, Dm->lv_inv.as<uint32_t>(), nullptr, nullptr, 0, st);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
 }
@@ -243,11 +243,11 @@ bh_status dist_h_phase3(bh_ctx* ctx, DistH& d, hipStream_t st) {
   uint32_t* b = a + d.M * 8;
   uint32_t* c = b + d.M * 8;
   // coset_fft's local M-point NTTs: DIF (natural q in, bit-reversed j out), omega_M
-  for (uint32_t* x : {a, b, c}) launch_ntt(x, d.Lm, true, Dm->tw_fwd.as<uint32_t>(), nullptr, nullptr, 0, st);
+  for (uint32_t* x : {a, b, c}) launch_ntt(x, d.Lm, true, Dm->lv_fwd.as<uint32_t>(), nullptr, nullptr, 0, st);
   // a*b - c, divide_by_z_on_coset (order-agnostic: the three vectors share the layout)
   launch_pointwise(a, b, c, d.M, 2, D->consts.as<uint32_t>() + 9, st);
   // icoset_fft's local iNTT_M: DIT (bit-reversed j in, natural q out), omega_M^-1
-  launch_ntt(a, d.Lm, false, Dm->tw_inv.as<uint32_t>(), nullptr, nullptr, 0, st);
+  launch_ntt(a, d.Lm, false, Dm->lv_inv.as<uint32_t>(), nullptr, nullptr, 0, st);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
 }

@@ -163,8 +163,8 @@ bh_status bh_multiexp_wait(bh_job* job, uint8_t* out) {
   const hipError_t e = hipEventSynchronize(sl->done);  // Waiter::wait: a host-side event sync
   bh_status s = e == hipSuccess ? BH_OK : BH_ERR_HIP;
   if (!s && out) {
-    if (j->group == BH_G1) g1_to_uncompressed(jac_to_affine(combine_g1(sl->ws1.host_window_sums, j->sh.Wb, j->sh.c)), out);
-    else g2_to_uncompressed(jac_to_affine(combine_g2(sl->ws2.host_window_sums, j->sh.Wb, j->sh.c)), out);
+    if (j->group == BH_G1) g1_to_uncompressed(jac_to_affine(combine_g1(sl->ws1.host_window_sums, j->sh)), out);
+    else g2_to_uncompressed(jac_to_affine(combine_g2(sl->ws2.host_window_sums, j->sh)), out);
   }
   give_slot(ctx, sl);
   if (!out && !s) return BH_ERR_INVALID_ARGUMENT;

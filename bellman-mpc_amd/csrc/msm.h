@@ -22,6 +22,23 @@ MsmShape msm_shape(size_t n, int c_override);
 int msm_table_c(size_t n);
 MsmShape msm_shape_table(size_t n, int c);
 
+// Bucket-reduction geometry (msm_back): L buckets per level-1 thread, blocks of
+// reduce_block_threads() threads.  With a single bucket window (Wb == 1) the device returns
+// two points and the host finishes the window: out[0] + 2^reduce_split_shift() * out[1]
+// (the shift's doublings are a serial chain: cheaper on the host than on one device thread).
+inline uint32_t reduce_block_threads(const MsmShape& sh, bool g2) {
+  const uint32_t T = (uint32_t)(sh.NB / sh.L), bmax = g2 ? 128u : 256u;
+  return T < bmax ? T : bmax;
+}
+inline int reduce_lg2(uint32_t x) {
+  int r = 0;
+  while ((1u << r) < x) r++;
+  return r;
+}
+inline int reduce_split_shift(const MsmShape& sh, bool g2) {
+  return sh.Wb == 1 ? reduce_lg2((uint32_t)sh.L) + reduce_lg2(reduce_block_threads(sh, g2)) : -1;
+}
+
 struct MsmTiming {
   hipEvent_t ev_acc_begin = nullptr, ev_acc_end = nullptr;  // bracket k_accumulate_dev
 };

@@ -214,9 +214,15 @@ MsmShape msm_shape(size_t n, int c_override) {
   sh.c = c;
   sh.W = (256 + c - 1) / c;
   sh.NB = 1 << (c - 1);
-  // buckets per reduction thread: 8 for large bucket sets (less segment-combine work), 4 below
-  // 2^18 buckets (more threads, shorter chains: the tail of a small shard is latency-bound)
-  sh.L = std::min<int>(sh.NB >= (1 << 18) ? 8 : 4, sh.NB);
+  // buckets per reduction thread (msm_back): 8 for large bucket sets (~3 additions per bucket;
+  // 16 would do less work, but its longer-lived waves cost the overlapped accumulations more:
+  // +2 ms per 2^22 proof in a same-box A/B), 4 below 2^15 (latency-bound small tails)
+  static const int l_big = [] {  // BH_REDUCE_L: the large-set value (A/B experiments)
+    const char* e = getenv("BH_REDUCE_L");
+    const int v = e ? atoi(e) : 8;
+    return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : 8;
+  }();
+  sh.L = std::min<int>(sh.NB >= (1 << 15) ? l_big : 4, sh.NB);
   size_t E = n * (size_t)sh.W;
   int S = 16;
   while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;
@@ -228,8 +234,8 @@ MsmShape msm_shape(size_t n, int c_override) {
 }
 
 // With a window table every digit window adds into one shared set of 2^(c-1) buckets, so
-// the accumulation costs n*ceil(256/c) mixed additions and the reduction ~6.5 * 2^(c-1)
-// (2 running-sum additions per bucket plus the segment combine), independent of W.
+// the accumulation costs n*ceil(256/c) mixed additions and the reduction ~3.6 * 2^(c-1)
+// mixed-addition equivalents (msm_back: ~2.6 full additions per bucket at L = 16), independent of W.
 // Only window sizes whose top window holds >= 10 real scalar bits: with shared buckets a
 // nearly empty top window (e.g. c = 17: the 16th window only takes the carry; c = 18: 3 bits)
 // pours up to n/2 entries into a handful of small-digit buckets, whose continuation partials
@@ -240,7 +246,7 @@ int msm_table_c(size_t n) {
   for (int c = 8; c <= 24; c++) {
     const int W = (256 + c - 1) / c;
     if (255 - (W - 1) * c < 10) continue;
-    const double cost = (double)n * W + 6.5 * (double)((size_t)1 << (c - 1));
+    const double cost = (double)n * W + 3.6 * (double)((size_t)1 << (c - 1));
     if (cost < best_cost) { best_cost = cost; best = c; }
   }
   return best;

@@ -147,62 +147,178 @@ __global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const 
   if (q == 0 && ncont >= 2) store_point<C>(&conts[s_first + 1], acc);
 }
 
-// Bucket reduction: thread (w, t) sums its L buckets by parts
-// (multiexp.rs:229-233 restricted to buckets [t*L, (t+1)*L)) and adds (t*L) * (their sum),
-// so out[w*T + t] = sum_{k<L} (t*L + k + 1) * B[t*L + k]  (bucket b holds digit b+1)
+// ---- Bucket reduction: window total  sum_{b < NB} (b+1) * B_b  (bucket b holds digit b+1;
+// multiexp.rs:225-235 computes it as one serial running sum per window).  Here it is a
+// two-level summation by parts with no scalar multiplications of partial sums:
+//   thread t of block `blk` (t = blk*BT + i) owns buckets [t*L, t*L + L):
+//     R_t = sum_k B,  A_t = sum_k (k+1) B          (2L additions, the running-sum idiom)
+//   then  sum_b (b+1) B_b = sum_t A_t + L * sum_t t R_t,  and inside a block
+//     sum_i (t0 + i) R = t0 * S_blk + sum_i V_i,   V_i = sum_{j > i} R_j (LDS suffix scan)
+//   so block blk emits Y_blk = sum_i (A_i + L*V_i) and S_blk = sum_i R_i, and
+//     window total = sum_blk Y_blk + (L*BT) * sum_blk blk * S_blk,
+//   the same shape one level up (k_reduce_window, one block per window).
+// Work ~ (2 + (log2 BT + log2 L) / L) additions per bucket; serial depth 2L + 2 log2 BT + log2 L.
+//
+// Each kernel is written as short programs of point operations with ONE addition and one
+// doubling call site (operands chosen per step): a G2 addition is ~20 000 instructions, and
+// every inlined copy would cost minutes of compile time.
+
 template <class C>
-__global__ void __launch_bounds__(64) k_bucket_combine(const uint32_t* counts, const uint32_t* offsets,
-                                                       const typename C::P* bucket_sums, const typename C::P* conts,
-                                                       uint32_t S, uint32_t NB, uint32_t L, uint32_t W,
-                                                       typename C::P* out) {
-  const uint32_t T = NB / L;
-  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= W * T) return;
-  const uint32_t w = gid / T, t = gid % T;
-  typename C::P running = C::identity(), acc = C::identity();
-  for (int k = (int)L - 1; k >= 0; k--) {
-    const uint32_t gb = w * NB + t * L + (uint32_t)k;
-    running = C::add(running, bucket_value<C>(gb, counts, offsets, bucket_sums, conts, S));
-    acc = C::add(acc, running);
-  }
-  const uint32_t k = t * L;
-  if (k != 0) {
-    typename C::P m = C::identity();
-    for (int bit = 31 - __clz(k); bit >= 0; bit--) {
-      m = C::dbl(m);
-      if ((k >> bit) & 1u) m = C::add(m, running);
-    }
-    acc = C::add(acc, m);
-  }
-  store_point<C>(&out[gid], acc);
+__device__ __forceinline__ typename C::P dbl_times(typename C::P v, int k) {
+  for (int j = 0; j < k; j++) v = C::dbl(v);
+  return v;
 }
 
-// Block-level sum: block (w, g) adds in[w][g*4B .. g*4B+4B) (B = blockDim: four points per
-// thread, then a B-way tree in LDS; B*sizeof(P) = 56 KB for G1 at B = 256, G2 at B = 128) into
-// out[w*Tout + g].  Two launches reduce up to 2^18 (G1) points.  With Tout == 1 the result is
-// written in canonical coordinates.
+// Block epilogue shared by both levels (lds: blockDim points, 2 * blockDim with split).  v = this thread's value:
+//   suffix scan over the block; V = sum_{j > i} v_j (exclusive suffix);
+//   x = base + 2^lg1 * V;
+//   compose (lg2 >= 0): x = extra + 2^lg2 * x, then the block sum of x;
+//   split   (lg2 <  0): the block sums of x and of extra side by side (two interleaved trees).
+// Thread 0 ends with lds[0] = sum x, lds[BT] = sum extra (split), *s_blk = sum v.
 template <class C>
-__global__ void __launch_bounds__(256) k_sum_tree(const typename C::P* in, uint32_t Tin, typename C::P* out,
-                                                  uint32_t Tout) {
-  extern __shared__ uint4 lds_raw[];
-  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
-  const uint32_t w = blockIdx.x / Tout, g = blockIdx.x % Tout;
-  const typename C::P* src = in + (size_t)w * Tin;
-  const uint32_t lo = g * 4u * blockDim.x + threadIdx.x * 4u;
-  typename C::P acc = C::identity();
-  for (uint32_t i = lo; i < min(lo + 4u, Tin); i++) acc = C::add(acc, load_point<C>(&src[i]));
-  store_point<C>(&lds[threadIdx.x], acc);
+__device__ __forceinline__ void block_epilogue(typename C::P v, const typename C::P& base, int lg1,
+                                               const typename C::P& extra, int lg2, bool split, typename C::P* lds,
+                                               typename C::P* s_blk) {
+  const uint32_t i = threadIdx.x, BT = blockDim.x;
+  int lgBT = 0;
+  while ((1u << lgBT) < BT) lgBT++;
+  const int n_final = lg2 >= 0 ? 2 : 1;
+  store_point<C>(&lds[i], v);
   __syncthreads();
-  for (uint32_t h = blockDim.x / 2; h > 0; h >>= 1) {
-    if (threadIdx.x < h) {
-      acc = C::add(acc, load_point<C>(&lds[threadIdx.x + h]));
-      store_point<C>(&lds[threadIdx.x], acc);
+  const int steps = 2 * lgBT + n_final;
+  for (int st = 0; st < steps; st++) {
+    typename C::P a = v, b;
+    bool act;
+    uint32_t dst = i;
+    if (st < lgBT) {  // suffix scan: v += v[i + 2^st]
+      const uint32_t d = 1u << st;
+      act = i + d < BT;
+      if (act) b = load_point<C>(&lds[i + d]);
+    } else if (st < lgBT + n_final) {  // x = base + 2^lg1 V, then x = extra + 2^lg2 x
+      const bool first = st == lgBT;
+      if (first) {
+        b = i + 1 < BT ? load_point<C>(&lds[i + 1]) : C::identity();
+        if (i == 0) *s_blk = load_point<C>(&lds[0]);
+      } else {
+        b = v;
+      }
+      b = dbl_times<C>(b, first ? lg1 : lg2);
+      a = first ? base : extra;
+      act = true;
+    } else {  // tree level with half size h: x-part on threads [0, h), extra-part on [h, 2h)
+      const uint32_t h = BT >> (st - lgBT - n_final + 1);
+      act = split ? i < 2 * h : i < h;
+      if (act) {
+        dst = i < h ? i : BT + (i - h);
+        a = load_point<C>(&lds[dst]);
+        b = load_point<C>(&lds[dst + h]);
+      }
     }
     __syncthreads();
+    if (act) {
+      v = C::add(a, b);
+      store_point<C>(&lds[dst], v);
+    }
+    if (split && st == lgBT + n_final - 1) store_point<C>(&lds[BT + i], extra);
+    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    if (Tout == 1) out[w] = C::reduce(acc);
-    else store_point<C>(&out[(size_t)w * Tout + g], acc);
+}
+
+// Level 1: grid = Wb * nblk blocks of BT threads (T = NB / L = nblk * BT); block
+// (w, blk) writes Y[w*nblk + blk] and S[w*nblk + blk].  A bucket spanning accumulation
+// segments s_first .. s_last has continuation partials conts[s_first+1 .. s_last]; with fold
+// they are all added here (short spans), else k_cont_seq / k_cont_treeF has already folded
+// them into conts[s_first+1].
+template <class C>
+__global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
+                                                       const typename C::P* bucket_sums, const typename C::P* conts,
+                                                       uint32_t S, uint32_t NB, uint32_t L, int lgL, uint32_t nblk,
+                                                       int fold, typename C::P* Y, typename C::P* Ssum) {
+  extern __shared__ uint4 lds_raw[];
+  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  const uint32_t i = threadIdx.x;
+  const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
+  const uint32_t gb0 = w * NB + (blk * blockDim.x + i) * L;
+  typename C::P run = C::identity(), acc = C::identity(), bk = C::identity();
+  // per bucket k = L-1 .. 0:  bk = partial (+ each continuation partial);  run += bk;  acc += run
+  int k = (int)L - 1;
+  uint32_t op = 0, c_next = 0, c_end = 0;  // op 0: load, 1: continuation, 2: run, 3: acc
+  while (k >= 0) {
+    typename C::P a, b;
+    if (op == 0) {
+      const uint32_t gb = gb0 + (uint32_t)k, cnt = counts[gb];
+      bk = C::identity();
+      c_next = c_end = 0;
+      if (cnt) {
+        bk = load_point<C>(&bucket_sums[gb]);
+        const uint32_t off = offsets[gb];
+        const uint32_t s_first = off / S, s_last = (off + cnt - 1) / S;
+        c_next = s_first + 1;
+        c_end = s_last > s_first ? (fold ? s_last + 1 : s_first + 2) : c_next;
+      }
+      op = c_next < c_end ? 1 : 2;
+      continue;
+    }
+    if (op == 1) { a = bk; b = load_point<C>(&conts[c_next]); }
+    else if (op == 2) { a = run; b = bk; }
+    else { a = acc; b = run; }
+    const typename C::P r = C::add(a, b);
+    if (op == 1) {
+      bk = r;
+      if (++c_next == c_end) op = 2;
+    } else if (op == 2) {
+      run = r;
+      op = 3;
+    } else {
+      acc = r;
+      op = 0;
+      k--;
+    }
+  }
+  typename C::P s_blk;
+  block_epilogue<C>(run, acc, lgL, acc, -1, false, lds, &s_blk);
+  if (i == 0) {
+    store_point<C>(&Y[blockIdx.x], load_point<C>(&lds[0]));
+    store_point<C>(&Ssum[blockIdx.x], s_blk);
+  }
+}
+
+// Level 2: one block of BT2 threads per window over its nblk = BT2 * Lb (Y, S) pairs:
+//   sum_blk Y + M * sum_blk blk * S,  M = 2^lgM = L * BT (level 1's block size)
+// thread j owns blocks [j*Lb, j*Lb + Lb): P_j = sum Y, A'_j = sum_k k S, R'_j = sum_k S, and
+//   sum_blk blk S = sum_j (A'_j + Lb * V'_j),  V'_j = sum_{j' > j} R'_j'
+// -> out[w] = the window total (canonical coordinates); split (one window): out[0] = sum P,
+// out[1] = sum_blk blk * S, and the host adds 2^lgM * out[1] (reduce_split_shift).
+template <class C>
+__global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
+                                                       uint32_t nblk, uint32_t Lb, int lgLb, int lgM, int split,
+                                                       typename C::P* out) {
+  extern __shared__ uint4 lds_raw[];
+  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  const uint32_t i = threadIdx.x, w = blockIdx.x;
+  const size_t base = (size_t)w * nblk + (size_t)i * Lb;
+  typename C::P run = C::identity(), acc = C::identity(), p = C::identity();
+  // per block k = Lb-1 .. 0:  acc += run;  run += S_k;  p += Y_k
+  for (uint32_t it = 0; it < 3 * Lb; it++) {
+    const uint32_t k = Lb - 1 - it / 3, op = it % 3;
+    typename C::P a, b;
+    if (op == 0) { a = acc; b = run; }
+    else if (op == 1) { a = run; b = load_point<C>(&Ssum[base + k]); }
+    else { a = p; b = load_point<C>(&Y[base + k]); }
+    const typename C::P r = C::add(a, b);
+    if (op == 0) acc = r;
+    else if (op == 1) run = r;
+    else p = r;
+  }
+  typename C::P s_unused;
+  block_epilogue<C>(run, acc, lgLb, p, split ? -1 : lgM, split != 0, lds, &s_unused);
+  if (i == 0) {
+    if (split) {
+      out[0] = C::reduce(load_point<C>(&lds[blockDim.x]));
+      out[1] = C::reduce(load_point<C>(&lds[0]));
+    } else {
+      out[w] = C::reduce(load_point<C>(&lds[0]));
+    }
   }
 }
 
@@ -473,41 +589,41 @@ template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
                     int max_span) {
   const size_t nbt = (size_t)sh.Wb * sh.NB;
-  // log-depth continuation fix-up: a bucket can span up to segs segments
+  // continuation partials: a bucket spanning up to REDUCE_FOLD_SPAN segments has them added
+  // by its reduction thread (no extra launch); longer spans (known from the sort) are folded
+  // first -- Q threads per bucket, or log-depth 4-ary tree levels
+  constexpr int REDUCE_FOLD_SPAN = 8;
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
-  if (max_span >= 0 && span <= cont_seq_max()) {
-    // short spans (known from the sort): Q threads per bucket fold its continuation partials
-    // -- one launch, about span/Q + log2(Q) serial additions
+  const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;
+  if (!fold && max_span >= 0 && span <= cont_seq_max()) {
     constexpr int Q = 4;
     constexpr uint32_t B = sizeof(typename C::P) > 256 ? 128 : 256;  // LDS: B points
     if (span >= 2)
       hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nbt * Q, B)), dim3(B), B * sizeof(typename C::P), st,
                          ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, ws.conts);
-  } else {
-    // a bucket owns at most span continuation partials: 4-ary tree levels, 3 serial additions each
+  } else if (!fold) {
     for (size_t stride = 1; stride < span; stride *= 4)
       hipLaunchKernelGGL((k_cont_treeF<C, 4>), dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
                          ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, (uint32_t)stride, ws.conts);
   }
-  const uint32_t T = (uint32_t)(sh.NB / sh.L);
-  const size_t total = (size_t)sh.Wb * T;
-  hipLaunchKernelGGL(k_bucket_combine<C>, dim3(msm_blocks_for(total, 64)), dim3(64), 0, st, ws.counts, ws.offsets,
-                     ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, (uint32_t)sh.L, (uint32_t)sh.Wb,
-                     ws.seg_weighted);
-  // seg_weighted -> seg_sum -> seg_weighted ... -> window_sums, 4*B points per block per level
-  constexpr uint32_t B = sizeof(typename C::P) > 256 ? 128 : 256;
-  typename C::P* bufs[2] = {ws.seg_weighted, ws.seg_sum};
-  uint32_t Tin = T;
-  for (int lvl = 0;; lvl++) {
-    const uint32_t Tout = (Tin + 4 * B - 1) / (4 * B);
-    typename C::P* dst = Tout == 1 ? ws.window_sums : bufs[(lvl + 1) & 1];
-    hipLaunchKernelGGL(k_sum_tree<C>, dim3((unsigned)(sh.Wb * Tout)), dim3(B), B * sizeof(typename C::P), st,
-                       bufs[lvl & 1], Tin, dst, Tout);
-    if (Tout == 1) break;
-    Tin = Tout;
-  }
-  hipMemcpyAsync(host_out, ws.window_sums, sh.Wb * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+  // two-level summation by parts (k_reduce_blocks, k_reduce_window): Y/S per level-1 block
+  // in seg_weighted / seg_sum, the window totals in window_sums
+  constexpr bool G2 = sizeof(typename C::P) > 256;
+  const uint32_t L = (uint32_t)sh.L;
+  const uint32_t T = (uint32_t)(sh.NB / L);
+  const uint32_t BT = reduce_block_threads(sh, G2);
+  const uint32_t nblk = T / BT;
+  const uint32_t BT2 = std::min(nblk, G2 ? 128u : 256u);
+  const uint32_t Lb = nblk / BT2;
+  const int split = reduce_split_shift(sh, G2) >= 0 ? 1 : 0;
+  hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
+                     ws.counts, ws.offsets, ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, L,
+                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted, ws.seg_sum);
+  hipLaunchKernelGGL(k_reduce_window<C>, dim3((unsigned)sh.Wb), dim3(BT2), 2 * BT2 * sizeof(typename C::P), st,
+                     ws.seg_weighted, ws.seg_sum, nblk, Lb, reduce_lg2(Lb), reduce_lg2(L) + reduce_lg2(BT), split,
+                     ws.window_sums);
+  hipMemcpyAsync(host_out, ws.window_sums, (split ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
   return hipGetLastError();
 }
 

@@ -11,12 +11,32 @@ struct FrConst {
   uint32_t v[9];  // raw 29-bit limbs
 };
 
-// In-place transform of 2^L packed Fr (device Montgomery, < 2r).
-// dif=true: natural -> bit-reversed; dif=false: bit-reversed -> natural.
-// tw: unpacked table omega^j, j < 2^(L-1).  post_lo/hi (optional): the stored
-// element with natural index i is multiplied by lo[i & mask] * hi[i >> lo_bits].
-void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* tw, const uint32_t* post_lo, const uint32_t* post_hi,
-                int post_lo_bits, hipStream_t st);
+// What the storing (last) pass of a transform writes, fused into it:
+//   STORE      : the transform, in place (d)
+//   AB_MINUS_C : the transform is c (natural order): pa[i] = (pa[i] * pb[i] - c[i]) * k[0]
+//                (prover.rs:221-225: a*b - c, divide_by_z_on_coset), c itself is not stored
+//   SCALARS    : out[nat] = canonical scalar of element nat for nat < n_out (prover.rs:227-231:
+//                truncate to m-1 and to_le_bits, natural order), the transform is not stored
+struct NttEpilogue {
+  enum Kind { STORE = 0, AB_MINUS_C = 1, SCALARS = 2 };
+  int kind = STORE;
+  uint32_t* pa = nullptr;
+  const uint32_t* pb = nullptr;
+  const uint32_t* k = nullptr;  // unpacked constant (9 limbs)
+  uint32_t* out = nullptr;
+  uint32_t n_out = 0;
+};
+
+// Transform of 2^L packed Fr (device Montgomery, < 2r) into d; the first pass reads src
+// (default: d, in place).  dif=true: natural -> bit-reversed; dif=false: bit-reversed -> natural.
+// lv: per-level packed twiddles lv[2^v + x] = omega_{2^(v+1)}^x (launch_level_table).
+// post_lo/hi (optional): the stored element with natural index i is multiplied by
+// lo[i & mask] * hi[i >> lo_bits].
+void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t* post_lo, const uint32_t* post_hi,
+                int post_lo_bits, hipStream_t st, const uint32_t* src = nullptr,
+                const NttEpilogue& epi = NttEpilogue());
+// lv (2^L packed entries) from the unpacked full table tw (omega^j, j < 2^(L-1))
+void launch_level_table(uint32_t* lv, int L, const uint32_t* tw, hipStream_t st);
 void launch_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo, const uint32_t* hi, int lo_bits,
                     hipStream_t st);
 void launch_scale(uint32_t* a, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits, const uint32_t* c,

@@ -16,6 +16,7 @@
 // that stores the data, indexed by the element's natural index.
 #include "ntt.h"
 #include "ntt_common.cuh"
+#include "msm.h"  // scalars_prepare (one-element epilogue)
 
 namespace bh {
 
@@ -25,10 +26,12 @@ static constexpr int NTT_T = 256;   // threads per workgroup
 
 struct PassArgs {
   int L, t, D;
-  const uint32_t* tw;     // omega^j, j < m/2 (unpacked)
+  const uint32_t* lv;       // per-level twiddles, packed: lv[2^v + x] = omega_{2^(v+1)}^x, x < 2^v
+  const uint32_t* src;      // loads come from src (the first pass may run out of place)
   const uint32_t* post_lo;  // optional post-scale tables
   const uint32_t* post_hi;
   int post_lo_bits;
+  NttEpilogue epi;          // what the storing pass writes
 };
 
 // global element index of (group g, position k) for a DIF pass at stages t..t+D-1
@@ -43,6 +46,11 @@ __device__ __forceinline__ uint32_t dit_index(const PassArgs& a, uint32_t g, uin
   return (hi << (a.t + a.D)) + (k << a.t) + lo;
 }
 
+// Twiddles: the butterfly of global stage u with in-level offset x uses omega_{2h}^x where h is
+// the stage's pair distance (DIT: h = 2^u, x = (k_low << t) + lo; DIF: h = 2^(L-u-1),
+// x = k_low * 2^(L-t-D) + lo).  With one packed table per level, lanes with consecutive lo
+// (consecutive groups) read consecutive 32-byte entries, and the level-0 stage (h = 1:
+// every twiddle is 1) multiplies by nothing.
 template <bool DIF>
 __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) {
   __shared__ uint32_t lds[9 * NTT_E];
@@ -61,7 +69,7 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
     const uint32_t g = g0 + gl;
     if (g >= total_groups) continue;
     const uint32_t idx = DIF ? dif_index(a, g, k) : dit_index(a, g, k);
-    DFr x = ld_packed(data, idx);
+    DFr x = ld_packed(a.src, idx);
     const uint32_t slot = (k << lgG) + gl;
 #pragma unroll
     for (int l = 0; l < 9; l++) lds[l * NTT_E + slot] = x.v[l];
@@ -70,10 +78,11 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
   // ---- D radix-2 stages
   for (int j = 0; j < D; j++) {
     const int u = a.t + j;  // global stage
+    const int hb = DIF ? (D - 1 - j) : j;  // pair distance 2^hb in k
+    const int v = DIF ? (a.L - u - 1) : u;  // twiddle level: omega_{2^(v+1)}
     for (uint32_t b = threadIdx.x; b < (uint32_t)(NTT_E / 2); b += NTT_T) {
       const uint32_t gl = b & (G - 1), r = b >> lgG;
       if (g0 + gl >= total_groups) continue;
-      const int hb = DIF ? (D - 1 - j) : j;  // pair distance 2^hb in k
       const uint32_t k = ((r >> hb) << (hb + 1)) | (r & ((1u << hb) - 1));
       const uint32_t k2 = k + (1u << hb);
       const uint32_t s0 = (k << lgG) + gl, s1 = (k2 << lgG) + gl;
@@ -81,31 +90,30 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
 #pragma unroll
       for (int l = 0; l < 9; l++) { x.v[l] = lds[l * NTT_E + s0]; y.v[l] = lds[l * NTT_E + s1]; }
       const uint32_t g = g0 + gl;
-      uint32_t e;
-      if (DIF) {
-        const uint32_t s = 1u << (a.L - a.t - D);
-        const uint32_t lo = g & (s - 1);
-        e = (((k & ((1u << hb) - 1)) * s) + lo) << u;
-      } else {
-        const uint32_t lo = g & ((1u << a.t) - 1);
-        e = (((k & ((1u << hb) - 1)) << a.t) + lo) << (a.L - u - 1);
-      }
-      const DFr w = ld_limbs(a.tw, e);
       DFr nx, ny;
-      if (DIF) {
+      if (v == 0) {  // omega_2^0 = 1
         nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
-        ny = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x, y), w);
+        ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, y));
       } else {
-        const DFr t = fe_mul<FrCfg>(y, w);
-        nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, t));
-        ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, t));
+        const uint32_t klow = k & ((1u << hb) - 1);
+        const uint32_t xo = DIF ? (klow << (a.L - a.t - D)) + (g & ((1u << (a.L - a.t - D)) - 1))
+                                : (klow << a.t) + (g & ((1u << a.t) - 1));
+        const DFr w = ld_packed(a.lv, (1u << v) + xo);
+        if (DIF) {
+          nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
+          ny = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x, y), w);
+        } else {
+          const DFr t = fe_mul<FrCfg>(y, w);
+          nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, t));
+          ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, t));
+        }
       }
 #pragma unroll
       for (int l = 0; l < 9; l++) { lds[l * NTT_E + s0] = nx.v[l]; lds[l * NTT_E + s1] = ny.v[l]; }
     }
     __syncthreads();
   }
-  // ---- store (+ optional post-scale by natural index)
+  // ---- store (+ optional post-scale by natural index, + the fused epilogue)
   for (uint32_t e = threadIdx.x; e < (uint32_t)NTT_E; e += NTT_T) {
     uint32_t gl, k;
     if (lo_fast) { gl = e & (G - 1); k = e >> lgG; } else { k = e & (K - 1); gl = e >> D; }
@@ -116,11 +124,24 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
     DFr x;
 #pragma unroll
     for (int l = 0; l < 9; l++) x.v[l] = lds[l * NTT_E + slot];
-    if (a.post_hi) {
-      const uint32_t nat = DIF ? brev(idx, a.L) : idx;
-      x = fe_mul<FrCfg>(x, pow_factor(a.post_lo, a.post_hi, a.post_lo_bits, nat));
+    const uint32_t nat = DIF ? brev(idx, a.L) : idx;
+    if (a.post_hi) x = fe_mul<FrCfg>(x, pow_factor(a.post_lo, a.post_hi, a.post_lo_bits, nat));
+    if (a.epi.kind == NttEpilogue::AB_MINUS_C) {  // x = c: pa[idx] = (pa[idx] * pb[idx] - x) * k
+      const DFr p = fe_mul<FrCfg>(ld_packed(a.epi.pa, idx), ld_packed(a.epi.pb, idx));
+      st_packed(a.epi.pa, idx, fe_mul<FrCfg>(fe_sub<FrCfg, 2>(p, x), ld_limbs(a.epi.k, 0)));
+    } else if (a.epi.kind == NttEpilogue::SCALARS) {  // canonical scalar at the natural index
+      if (nat < a.epi.n_out) {
+        DFr one = fe_zero<FrCfg>();
+        one.v[0] = 1u;  // x * 1 * 2^-261: out of device Montgomery form
+        uint32_t w8[8];
+        fe_pack<FrCfg>(fe_reduce_full<FrCfg>(fe_mul<FrCfg>(x, one)), w8);
+        uint4* q = reinterpret_cast<uint4*>(a.epi.out + (size_t)nat * 8);
+        q[0] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
+        q[1] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
+      }
+    } else {
+      st_packed(data, idx, x);
     }
-    st_packed(data, idx, x);
   }
 }
 
@@ -185,14 +206,28 @@ __global__ void __launch_bounds__(256) k_expand_table(uint32_t* tab, uint32_t n,
   for (int l = 0; l < 9; l++) tab[(size_t)j * 9 + l] = x.v[l];
 }
 
+// per-level twiddles from the full table: lv[2^v + x] = omega^(x * 2^(L-1-v)) (packed), v < L
+__global__ void __launch_bounds__(256) k_level_table(uint32_t* lv, int L, const uint32_t* tw) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0 || e >= (1u << L)) return;
+  const int v = 31 - __clz(e);
+  const uint32_t x = e - (1u << v);
+  st_packed(lv, e, ld_limbs(tw, (size_t)x << (L - 1 - v)));
+}
+
 // ------------------------------------------------------------------ host side
 static inline unsigned nb(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* tw, const uint32_t* post_lo, const uint32_t* post_hi,
-                int post_lo_bits, hipStream_t st) {
-  if (L == 0) {
+void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t* post_lo, const uint32_t* post_hi,
+                int post_lo_bits, hipStream_t st, const uint32_t* src, const NttEpilogue& epi) {
+  if (L == 0) {  // one element: a copy, the post-scale and the epilogue
+    if (src && src != d) hipMemcpyAsync(d, src, 32, hipMemcpyDeviceToDevice, st);
     if (post_hi) hipLaunchKernelGGL(k_scale, dim3(1), dim3(256), 0, st, d, 1u, post_lo, post_hi, post_lo_bits,
                                     (const uint32_t*)nullptr);
+    if (epi.kind == NttEpilogue::AB_MINUS_C)
+      hipLaunchKernelGGL(k_pointwise, dim3(1), dim3(256), 0, st, epi.pa, epi.pb, (const uint32_t*)d, 1u, 2, epi.k);
+    else if (epi.kind == NttEpilogue::SCALARS && epi.n_out)
+      scalars_prepare(d, epi.out, epi.n_out, 2, 0, st);
     return;
   }
   const int passes = (L + 9) / 10;
@@ -201,11 +236,13 @@ void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* tw, const uint32_t
   int t = 0;
   for (int p = 0; p < passes; p++) {
     PassArgs a;
-    a.L = L; a.t = t; a.D = Ds[p]; a.tw = tw;
+    a.L = L; a.t = t; a.D = Ds[p]; a.lv = lv;
     const bool last = (p == passes - 1);
+    a.src = (p == 0 && src) ? src : d;
     a.post_lo = last ? post_lo : nullptr;
     a.post_hi = last ? post_hi : nullptr;
     a.post_lo_bits = post_lo_bits;
+    a.epi = last ? epi : NttEpilogue();
     const size_t groups = (size_t)1 << (L - a.D);
     const size_t G = NTT_E >> a.D;
     const unsigned blocks = (unsigned)((groups + G - 1) / G);
@@ -237,6 +274,10 @@ void launch_expand_table(uint32_t* tab, size_t n, const uint32_t* lo, const uint
                          hipStream_t st) {
   if (!n) return;
   hipLaunchKernelGGL(k_expand_table, dim3(nb(n, 256)), dim3(256), 0, st, tab, (uint32_t)n, lo, hi, lo_bits);
+}
+void launch_level_table(uint32_t* lv, int L, const uint32_t* tw, hipStream_t st) {
+  if (L < 1) return;
+  hipLaunchKernelGGL(k_level_table, dim3(nb((size_t)1 << L, 256)), dim3(256), 0, st, lv, L, tw);
 }
 
 }  // namespace bh

@@ -716,6 +716,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (!up->wait(2)) return up->status;
       BH_TRY_HIP(hipStreamWaitEvent(sH, up->ev[1], 0));
     }
+    const uint32_t* src = w->abc.as<uint32_t>();  // the first passes read the witness in place
     if (w->raw) {  // convert into the H block's buffer (bls12_381 -> device Montgomery), zero padding
       const size_t nc = w->num_constraints;
       for (int v = 0; v < 3; v++) {
@@ -724,13 +725,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
         if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
       }
       BH_TRY_HIP(hipGetLastError());
-    } else {
-      BH_TRY_HIP(hipMemcpyAsync(abc, w->abc.p, 3 * m * 32, hipMemcpyDeviceToDevice, sH));
+      src = nullptr;
     }
-    bh_status hs = run_h_pipeline(ctx, D, abc, sH);
+    // ... and the last one writes h as canonical scalars in natural order, truncated to m-1
+    // (prover.rs:227-231)
+    bh_status hs = run_h_pipeline(ctx, D, abc, sH, src, ctx->hbuf.as<uint32_t>());
     if (hs) return hs;
-    // truncate to m-1 and convert to canonical scalars in natural order (prover.rs:227-231)
-    BH_TRY_HIP(scalars_prepare(abc, ctx->hbuf.as<uint32_t>(), m - 1, 2, L, sH));
     hipEventRecord(ctx->ev[1], sH);
     return BH_OK;
   };
@@ -876,13 +876,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (jobs[big[q]].is_h) h_pos = q;
   // The last accumulated multiexp's reduction tail runs alone on an idle GPU, at the end of
   // the critical path: give its bucket reduction more, shorter chains (fewer buckets per
-  // thread, down to one: ~22 instead of ~34 serial point operations at 2^15 buckets), while
+  // thread: 2L + 2 log2(BT) + log2(L) serial point operations in k_reduce_blocks), while
   // the earlier tails, which share the SIMDs with accumulations, keep the work-lean shape.
   if (nbig > 0) {
     MsmShape& sl = shapes[big[nbig - 1]];
     static const int last_threads = [] {
       const char* e = getenv("BH_LAST_TAIL_THREADS");
-      return e ? atoi(e) : 32768;
+      return e ? atoi(e) : 65536;
     }();
     if (last_threads > 0) {
       int L = sl.L;
@@ -976,10 +976,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (acc_events_on()) (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
     const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
     if (J.g2) {
-      res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j].Wb, shapes[j].c);
+      res2[J.out] = combine_g2(ctx->host_out2 + 128 * J.out, shapes[j]);
       g2_acc_ms += t; g2_launches++; g2_pairs += pairs; g2_adds += ctx->host_counts[j];
     } else {
-      res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j].Wb, shapes[j].c);
+      res1[J.out] = combine_g1(ctx->host_out1 + 128 * J.out, shapes[j]);
       g1_acc_ms += t; g1_launches++; g1_pairs += pairs; g1_adds += ctx->host_counts[j];
     }
   }
