@@ -619,10 +619,17 @@ int bh_version(void) { return 1; }
 
 // The prover keeps 12 streams in flight (accumulations, sorts, H, small multiexps and one
 // reduction tail per large multiexp).  HIP maps streams onto GPU_MAX_HW_QUEUES hardware
-// queues (default 4); streams sharing a queue serialise behind each other's event waits,
-// which would queue every tail behind the next accumulation.  Ask for 16 queues unless the
-// host already chose a value; this runs when the library is loaded, before any HIP call.
-__attribute__((constructor)) static void bh_hw_queues() { setenv("GPU_MAX_HW_QUEUES", "16", 0); }
+// queues (4 by default); streams sharing a queue serialise behind each other's work: with 4,
+// a reduction tail waits behind another multiexp's tail, and the sort and H streams behind
+// tails (measured in a kernel trace: queue ids shared by streams 6/7, 4/9, 5/8).  Raise the
+// value to 16 when it is lower (BH_KEEP_HW_QUEUES=1 keeps the environment's value); this runs
+// when the library is loaded, before the runtime reads it at its first HIP call.
+__attribute__((constructor)) static void bh_hw_queues() {
+  const char* keep = getenv("BH_KEEP_HW_QUEUES");
+  if (keep && keep[0] == '1') return;
+  const char* cur = getenv("GPU_MAX_HW_QUEUES");
+  if (!cur || atoi(cur) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+}
 
 bh_status bh_ctx_create(int device, bh_ctx** out) {
   if (!out) return BH_ERR_INVALID_ARGUMENT;
@@ -648,11 +655,40 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     delete c;
     return BH_ERR_HIP;
   }
-  for (auto& t : c->tstream)
-    if (hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess) {
+  // The reduction tails run on a quarter of the CUs (every 4th, a CU mask): their waves are
+  // latency-bound chains of point additions that would otherwise hold SIMD slots of the
+  // accumulations on every CU (same-box A/B at 2^22: -0.5 to -0.8 ms per proof with 64 of 256
+  // CUs; 32 or 96 were no better).  BH_TAIL_CUS = k overrides (0: no mask); BH_SORT_CUS and
+  // BH_H_CUS do the same for the sort and H streams (A/B experiments, default unmasked).
+  int ncu = 0;
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  auto masked = [&](const char* var, hipStream_t* st) -> int {  // 1 created, 0 not asked, -1 error
+    const char* e = getenv(var);
+    const bool tails = strcmp(var, "BH_TAIL_CUS") == 0;
+    const int k = e ? atoi(e) : (tails ? ncu / 4 : 0);
+    if (k <= 0 || ncu <= 0 || k >= ncu) return 0;
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    const int step = ncu / k;
+    for (int i = 0, got = 0; i < ncu && got < k; i++)
+      if (i % step == step - 1) { mask[(size_t)i / 32] |= 1u << (i % 32); got++; }
+    return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess ? 1 : -1;
+  };
+  for (auto& t : c->tstream) {
+    const int r = masked("BH_TAIL_CUS", &t);
+    if (r < 0 || (r == 0 && hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess)) {
       delete c;
       return BH_ERR_HIP;
     }
+  }
+  for (hipStream_t* sp : {&c->stream3, &c->stream4}) {
+    hipStream_t m = nullptr;
+    const int r = masked(sp == &c->stream3 ? "BH_SORT_CUS" : "BH_H_CUS", &m);
+    if (r < 0) { delete c; return BH_ERR_HIP; }
+    if (r > 0) {
+      (void)hipStreamDestroy(*sp);
+      *sp = m;
+    }
+  }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)

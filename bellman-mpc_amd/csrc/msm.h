@@ -26,8 +26,9 @@ MsmShape msm_shape_table(size_t n, int c);
 // reduce_block_threads() threads.  With a single bucket window (Wb == 1) the device returns
 // two points and the host finishes the window: out[0] + 2^reduce_split_shift() * out[1]
 // (the shift's doublings are a serial chain: cheaper on the host than on one device thread).
+uint32_t reduce_block_max(bool g2);  // BH_REDUCE_BT (A/B), default 256 (G1) / 128 (G2)
 inline uint32_t reduce_block_threads(const MsmShape& sh, bool g2) {
-  const uint32_t T = (uint32_t)(sh.NB / sh.L), bmax = g2 ? 128u : 256u;
+  const uint32_t T = (uint32_t)(sh.NB / sh.L), bmax = reduce_block_max(g2);
   return T < bmax ? T : bmax;
 }
 inline int reduce_lg2(uint32_t x) {

@@ -214,15 +214,22 @@ MsmShape msm_shape(size_t n, int c_override) {
   sh.c = c;
   sh.W = (256 + c - 1) / c;
   sh.NB = 1 << (c - 1);
-  // buckets per reduction thread (msm_back): 8 for large bucket sets (~3 additions per bucket;
-  // 16 would do less work, but its longer-lived waves cost the overlapped accumulations more:
-  // +2 ms per 2^22 proof in a same-box A/B), 4 below 2^15 (latency-bound small tails)
+  // buckets per reduction thread (msm_back): up to 8 (~3 additions per bucket; 16 would do less
+  // work, but its longer-lived waves cost the overlapped accumulations more: +2 ms per 2^22
+  // proof in a same-box A/B), fewer when that leaves under 16384 threads (a small bucket set's
+  // tail is latency-bound: a shard's G2 tail at 2^15 buckets took 5.8 ms beside the
+  // accumulations with L = 8, 4096 threads)
   static const int l_big = [] {  // BH_REDUCE_L: the large-set value (A/B experiments)
     const char* e = getenv("BH_REDUCE_L");
     const int v = e ? atoi(e) : 8;
     return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : 8;
   }();
-  sh.L = std::min<int>(sh.NB >= (1 << 15) ? l_big : 4, sh.NB);
+  static const size_t t_min = [] {  // BH_REDUCE_TMIN: minimum reduction threads
+    const char* e = getenv("BH_REDUCE_TMIN");
+    return e ? (size_t)atol(e) : (size_t)16384;
+  }();
+  sh.L = std::min<int>(l_big, sh.NB);
+  while (sh.L > 1 && (size_t)sh.W * (size_t)(sh.NB / sh.L) < t_min) sh.L >>= 1;
   size_t E = n * (size_t)sh.W;
   int S = 16;
   while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;
@@ -240,7 +247,23 @@ MsmShape msm_shape(size_t n, int c_override) {
 // nearly empty top window (e.g. c = 17: the 16th window only takes the carry; c = 18: 3 bits)
 // pours up to n/2 entries into a handful of small-digit buckets, whose continuation partials
 // then need the log-depth tree (msm_back).  For 255-bit scalars: c = 16, 20, 22, 24.
+uint32_t reduce_block_max(bool g2) {
+  static const uint32_t v = [] {
+    const char* e = getenv("BH_REDUCE_BT");
+    const long x = e ? atol(e) : 0;
+    return (x == 64 || x == 128 || x == 256) ? (uint32_t)x : 0u;
+  }();
+  if (v) return g2 ? std::min<uint32_t>(v, 128u) : v;
+  return g2 ? 128u : 256u;
+}
+
 int msm_table_c(size_t n) {
+  static const int forced = [] {  // BH_TABLE_C: force the table window size (A/B experiments)
+    const char* e = getenv("BH_TABLE_C");
+    const int v = e ? atoi(e) : 0;
+    return (v == 16 || v == 20 || v == 22 || v == 24) ? v : 0;
+  }();
+  if (forced) return forced;
   int best = 16;
   double best_cost = 1e300;
   for (int c = 8; c <= 24; c++) {
@@ -256,6 +279,12 @@ MsmShape msm_shape_table(size_t n, int c) {
   MsmShape sh = msm_shape(n, c);
   sh.Wb = 1;
   sh.pre = 1;
+  // one shared bucket window: the reduction's thread count is NB / L
+  static const size_t t_min = [] {
+    const char* e = getenv("BH_REDUCE_TMIN");
+    return e ? (size_t)atol(e) : (size_t)16384;
+  }();
+  while (sh.L > 1 && (size_t)(sh.NB / sh.L) < t_min) sh.L >>= 1;
   return sh;
 }
 

@@ -417,10 +417,17 @@ void fit_segments(MsmShape& sh, size_t n) {
     const double f = e ? atof(e) : 1.0;
     return (f > 0.0 && f <= 1.0) ? f : 1.0;
   }();
+  // BH_ACC_MIN_S: floor of the segment length (short segments multiply the continuation
+  // partials and the per-segment bucket search)
+  static const size_t min_s = [] {
+    const char* e = getenv("BH_ACC_MIN_S");
+    const long v = e ? atol(e) : 8;
+    return (size_t)(v >= 1 ? v : 8);
+  }();
   const size_t E = n * (size_t)sh.W;
   const size_t slots = std::max<size_t>((size_t)(rounds * conc * fill) / 256 * 256, 256);
   size_t S = (E + slots - 1) / slots;
-  sh.S = (int)std::min<size_t>(std::max<size_t>(S, 8), (size_t)1 << 16);
+  sh.S = (int)std::min<size_t>(std::max<size_t>(S, min_s), (size_t)1 << 16);
 }
 
 template <class C>

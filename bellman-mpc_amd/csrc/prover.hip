@@ -562,6 +562,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                        Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
                        UploadSync* up = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
+  // an error return in the middle of enqueueing leaves kernels running on the streams below,
+  // reading workspaces the next call reuses: drain every stream before returning one
+  struct DrainOnError {
+    bh_ctx* c;
+    bool ok = false;
+    ~DrainOnError() { if (!ok) ctx_sync_all(c); }
+  } drain{ctx};
   bh_params* mparams = const_cast<bh_params*>(params);
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
   const int L = w->log_m;
@@ -1011,6 +1018,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
               params->b_g2.win.bytes;
   for (const auto& kv : params->h_shares) tb += kv.second->win.bytes;
   ctx->last_timings[12] = (double)tb;
+  drain.ok = true;
   return BH_OK;
 }
 
@@ -1347,7 +1355,22 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
   // on `lanes` contexts of this device, each driven by a host thread through a share of the
   // batch, so one proof's start-up (sorts, H) and reduction tails fill the bubbles of
   // another's accumulations; proofs_out[i] is exactly bh_prove_witness(ws[i]).
-  const int L = (int)std::min<size_t>(lanes ? (size_t)lanes : 2, k);
+  const int L = (int)std::min<size_t>(lanes ? (size_t)lanes : 1, k);
+  if (L == 1) {
+    // one lane: the proofs back to back on this context.  A proof already fills the device
+    // (same-box A/B at 2^20: 19.7 ms per proof with one lane, 19.8 with two, 21.6 with three),
+    // and every extra context adds 13 streams, i.e. hardware queues: beyond the 16 the library
+    // asks for, queues time-share and a proof takes ~33 ms.
+    const VkHost vk1 = vk_of(params);
+    for (size_t i = 0; i < k; i++) {
+      Jac<Fp> r1[6];
+      Jac<bh::Fp2> r2[2];
+      bh_status st1 = compute_msms_sync(ctx, params, ws[i], 0, 1, r1, r2, nullptr, true);
+      if (st1) return st1;
+      assemble(vk1, r1, r2, r_in, s_in, proofs_out + 192 * i);
+    }
+    return BH_OK;
+  }
   while ((int)ctx->lanes.size() < L) {
     bh_ctx* v = nullptr;
     bh_status st = bh_ctx_create(ctx->device, &v);

@@ -162,10 +162,13 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
                            const uint64_t s[4], uint8_t proof_out[192]);
 
 /* Throughput mode (BASELINE.json configs[4], "C5"): k independent proofs of witnesses sharing
- * one Parameters, pipelined on `lanes` streams-and-workspace sets of this device (0 = default,
- * 2) so that one proof's sorts, H block and reduction tails fill the gaps of another's
- * accumulations.  proofs_out: k * 192 bytes, proof i == bh_prove_witness(ws[i]).  Across GPUs
- * the batch is split by the caller (one process per GPU, no collective). */
+ * one Parameters (the reference's Worker::compute fan-out, multicore.rs:33-76, r and s fixed,
+ * prover.rs:158-173), every window table built once up front.  lanes (0 = default, 1): with 1
+ * the proofs run back to back on ctx (a 2^20 proof already fills the device); with more, on
+ * that many contexts of this device driven by host threads, so one proof's sorts, H block and
+ * tails overlap another's accumulations (each context adds hardware queues: measured slower).
+ * proofs_out: k * 192 bytes, proof i == bh_prove_witness(ws[i]).  Across GPUs the batch is
+ * split by the caller (one process per GPU, no collective). */
 bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
                          const uint64_t r[4], const uint64_t s[4], int lanes, uint8_t* proofs_out);
 
