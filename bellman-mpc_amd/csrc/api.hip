@@ -5,6 +5,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 
@@ -631,6 +632,12 @@ __attribute__((constructor)) static void bh_hw_queues() {
   if (!cur || atoi(cur) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
 }
 
+static std::atomic<int> g_masked_ctxs[64];  // live CU-masked contexts per device (0 or 1)
+static void release_mask(bh_ctx* c) {
+  if (c->cu_masked) g_masked_ctxs[c->device].fetch_sub(1);
+  c->cu_masked = false;
+}
+
 bh_status bh_ctx_create(int device, bh_ctx** out) {
   if (!out) return BH_ERR_INVALID_ARGUMENT;
   int count = 0;
@@ -660,9 +667,15 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   // accumulations on every CU (same-box A/B at 2^22: -0.5 to -0.8 ms per proof with 64 of 256
   // CUs; 32 or 96 were no better).  BH_TAIL_CUS = k overrides (0: no mask); BH_SORT_CUS and
   // BH_H_CUS do the same for the sort and H streams (A/B experiments, default unmasked).
+  // A CU-masked stream takes a hardware queue of its own: only the first live context of a
+  // device masks (virtual ranks and extra lanes are further contexts; 8 of them with 8 masked
+  // tail queues each oversubscribed the queues and one rank never ran -- a hang).
   int ncu = 0;
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+  c->cu_masked = device >= 0 && device < 64 && g_masked_ctxs[device].fetch_add(1) == 0;
+  if (!c->cu_masked && device >= 0 && device < 64) g_masked_ctxs[device].fetch_sub(1);
   auto masked = [&](const char* var, hipStream_t* st) -> int {  // 1 created, 0 not asked, -1 error
+    if (!c->cu_masked) return 0;
     const char* e = getenv(var);
     const bool tails = strcmp(var, "BH_TAIL_CUS") == 0;
     const int k = e ? atoi(e) : (tails ? ncu / 4 : 0);
@@ -676,27 +689,27 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   for (auto& t : c->tstream) {
     const int r = masked("BH_TAIL_CUS", &t);
     if (r < 0 || (r == 0 && hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess)) {
-      delete c;
+      release_mask(c); delete c;
       return BH_ERR_HIP;
     }
   }
   for (hipStream_t* sp : {&c->stream3, &c->stream4}) {
     hipStream_t m = nullptr;
     const int r = masked(sp == &c->stream3 ? "BH_SORT_CUS" : "BH_H_CUS", &m);
-    if (r < 0) { delete c; return BH_ERR_HIP; }
+    if (r < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
     if (r > 0) {
       (void)hipStreamDestroy(*sp);
       *sp = m;
     }
   }
   for (auto& e : c->ev)
-    if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
+    if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
-    if (hipEventCreate(&e) != hipSuccess) { delete c; return BH_ERR_HIP; }
+    if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-    delete c;
+    release_mask(c); delete c;
     return BH_ERR_OUT_OF_MEMORY;
   }
   *out = c;
@@ -733,6 +746,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream4);
   for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
+  release_mask(ctx);
   delete ctx->dist;
   delete ctx;
   return BH_OK;

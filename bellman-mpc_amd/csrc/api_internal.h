@@ -128,6 +128,7 @@ struct bh_witness {
 
 struct bh_ctx {
   int device = 0;
+  bool cu_masked = false;  // its tail streams are CU-masked (the first live context of a device)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)

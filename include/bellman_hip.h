@@ -82,7 +82,7 @@ bh_status bh_ctx_reserve(bh_ctx* ctx, size_t max_msm_len, uint32_t max_log_domai
 bh_status bh_ctx_set_window(bh_ctx* ctx, int c);
 /* Prover SRS window tables (default 1 = on): for each large query of the Parameters the
  * prover keeps T[i*W + w] = 2^(c*w) * P_i resident in HBM (built once per Parameters,
- * ~42 GB at 2^22 constraints on one GPU, 1/N of that per rank of an N-GPU run; skipped, with
+ * ~31 GB at 2^22 constraints on one GPU, 1/N of that per rank of an N-GPU run; skipped, with
  * a message on stderr, when HBM is short) so that all digit windows share one bucket set and
  * c can grow.  Results never depend on it. */
 bh_status bh_ctx_set_tables(bh_ctx* ctx, int enable);
