@@ -75,10 +75,17 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
     for (int l = 0; l < 9; l++) lds[l * NTT_E + slot] = x.v[l];
   }
   __syncthreads();
-  // ---- D radix-2 stages
-  for (int j = 0; j < D; j++) {
-    const int u = a.t + j;  // global stage
-    const int hb = DIF ? (D - 1 - j) : j;  // pair distance 2^hb in k
+  // ---- D stages: one radix-2 stage when D is odd (DIF: the first, DIT: the first), then radix-4
+  // steps of two stages each in registers (half the LDS round trips, barriers and index math of
+  // two radix-2 stages, three twiddle loads instead of four; the same four products)
+  const int lo_bits = DIF ? (a.L - a.t - D) : a.t;  // bits of the group index below the k digits
+  auto twiddle = [&](int v, uint32_t klow, uint32_t g) -> DFr {  // omega_{2^(v+1)}^(klow * 2^lo_bits + lo)
+    return ld_packed(a.lv, (1u << v) + (klow << lo_bits) + (g & ((1u << lo_bits) - 1)));
+  };
+  int j = 0;
+  if (D & 1) {
+    const int u = a.t;  // global stage
+    const int hb = DIF ? (D - 1) : 0;  // pair distance 2^hb in k
     const int v = DIF ? (a.L - u - 1) : u;  // twiddle level: omega_{2^(v+1)}
     for (uint32_t b = threadIdx.x; b < (uint32_t)(NTT_E / 2); b += NTT_T) {
       const uint32_t gl = b & (G - 1), r = b >> lgG;
@@ -89,27 +96,99 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
       DFr x, y;
 #pragma unroll
       for (int l = 0; l < 9; l++) { x.v[l] = lds[l * NTT_E + s0]; y.v[l] = lds[l * NTT_E + s1]; }
-      const uint32_t g = g0 + gl;
       DFr nx, ny;
       if (v == 0) {  // omega_2^0 = 1
         nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
         ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, y));
       } else {
-        const uint32_t klow = k & ((1u << hb) - 1);
-        const uint32_t xo = DIF ? (klow << (a.L - a.t - D)) + (g & ((1u << (a.L - a.t - D)) - 1))
-                                : (klow << a.t) + (g & ((1u << a.t) - 1));
-        const DFr w = ld_packed(a.lv, (1u << v) + xo);
+        const DFr w = twiddle(v, k & ((1u << hb) - 1), g0 + gl);
         if (DIF) {
           nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
           ny = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x, y), w);
-        } else {
+        } else {  // lazy: no conditional subtraction inside a DIT pass (see the store)
           const DFr t = fe_mul<FrCfg>(y, w);
-          nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, t));
-          ny = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, t));
+          nx = fe_add<FrCfg>(x, t);
+          ny = fe_sub<FrCfg, 2>(x, t);
         }
       }
 #pragma unroll
       for (int l = 0; l < 9; l++) { lds[l * NTT_E + s0] = nx.v[l]; lds[l * NTT_E + s1] = ny.v[l]; }
+    }
+    __syncthreads();
+    j = 1;
+  }
+  for (; j < D; j += 2) {
+    const int u = a.t + j;                  // first of the two global stages
+    const int hb = DIF ? (D - 1 - j) : j;   // DIF: distances 2^hb, 2^(hb-1); DIT: 2^hb, 2^(hb+1)
+    const int lo2 = DIF ? hb - 1 : hb;      // the two k bits are lo2 and lo2 + 1
+    for (uint32_t b = threadIdx.x; b < (uint32_t)(NTT_E / 4); b += NTT_T) {
+      const uint32_t gl = b & (G - 1), r = b >> lgG;
+      const uint32_t g = g0 + gl;
+      if (g >= total_groups) continue;
+      const uint32_t k0 = ((r >> lo2) << (lo2 + 2)) | (r & ((1u << lo2) - 1));
+      const uint32_t ks[4] = {k0, k0 + (1u << lo2), k0 + (2u << lo2), k0 + (3u << lo2)};
+      DFr x[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t sl = (ks[q] << lgG) + gl;
+#pragma unroll
+        for (int l = 0; l < 9; l++) x[q].v[l] = lds[l * NTT_E + sl];
+      }
+      DFr y[4];
+      if (DIF) {
+        // stage u (distance 2^hb): (k0, k2), (k1, k3); stage u+1 (2^(hb-1)): (k0, k1), (k2, k3)
+        const int v = a.L - u - 1, v2 = v - 1;
+        const uint32_t m1 = (1u << hb) - 1, m2 = (1u << (hb - 1)) - 1;
+        const DFr wa0 = twiddle(v, ks[0] & m1, g), wa1 = twiddle(v, ks[1] & m1, g);
+        const DFr u0 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[0], x[2]));
+        const DFr u2 = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x[0], x[2]), wa0);
+        const DFr u1 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[1], x[3]));
+        const DFr u3 = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x[1], x[3]), wa1);
+        y[0] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u0, u1));
+        y[2] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u2, u3));
+        if (v2 == 0) {  // omega_2^0 = 1
+          y[1] = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(u0, u1));
+          y[3] = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(u2, u3));
+        } else {
+          const DFr wb = twiddle(v2, ks[0] & m2, g);
+          y[1] = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(u0, u1), wb);
+          y[3] = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(u2, u3), wb);
+        }
+      } else {
+        // stage u (distance 2^hb): (k0, k1), (k2, k3); stage u+1 (2^(hb+1)): (k0, k2), (k1, k3).
+        // Lazy reduction: a DIT stage adds a product (< 2r) to, or subtracts it (+2r) from, a value
+        // < B, so values stay < 2r(D+1) <= 22r < 2^261 in the 9 limbs, and a Montgomery product
+        // of such a value with a twiddle (< r) still ends < 2r (22 r^2 < 2^261 r); the storing
+        // pass reduces.  v == 0 only occurs at global stage 0, on freshly loaded values (< 2r).
+        const int v = u, v2 = u + 1;
+        const uint32_t m1 = (1u << hb) - 1, m2 = (2u << hb) - 1;
+        DFr u0, u1, u2, u3;
+        if (v == 0) {  // omega_2^0 = 1
+          u0 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[0], x[1]));
+          u1 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[0], x[1]));
+          u2 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[2], x[3]));
+          u3 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[2], x[3]));
+        } else {
+          const DFr wa = twiddle(v, ks[0] & m1, g);
+          const DFr t0 = fe_mul<FrCfg>(x[1], wa), t1 = fe_mul<FrCfg>(x[3], wa);
+          u0 = fe_add<FrCfg>(x[0], t0);
+          u1 = fe_sub<FrCfg, 2>(x[0], t0);
+          u2 = fe_add<FrCfg>(x[2], t1);
+          u3 = fe_sub<FrCfg, 2>(x[2], t1);
+        }
+        const DFr wb0 = twiddle(v2, ks[0] & m2, g), wb1 = twiddle(v2, ks[1] & m2, g);
+        const DFr s0 = fe_mul<FrCfg>(u2, wb0), s1 = fe_mul<FrCfg>(u3, wb1);
+        y[0] = fe_add<FrCfg>(u0, s0);
+        y[2] = fe_sub<FrCfg, 2>(u0, s0);
+        y[1] = fe_add<FrCfg>(u1, s1);
+        y[3] = fe_sub<FrCfg, 2>(u1, s1);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t sl = (ks[q] << lgG) + gl;
+#pragma unroll
+        for (int l = 0; l < 9; l++) lds[l * NTT_E + sl] = y[q].v[l];
+      }
     }
     __syncthreads();
   }
@@ -125,10 +204,10 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
 #pragma unroll
     for (int l = 0; l < 9; l++) x.v[l] = lds[l * NTT_E + slot];
     const uint32_t nat = DIF ? brev(idx, a.L) : idx;
-    if (a.post_hi) x = fe_mul<FrCfg>(x, pow_factor(a.post_lo, a.post_hi, a.post_lo_bits, nat));
-    if (a.epi.kind == NttEpilogue::AB_MINUS_C) {  // x = c: pa[idx] = (pa[idx] * pb[idx] - x) * k
+    if (a.post_hi) x = fe_mul<FrCfg>(x, pow_factor(a.post_lo, a.post_hi, a.post_lo_bits, nat));  // < 2r
+    if (a.epi.kind == NttEpilogue::AB_MINUS_C) {  // x = c (< 22r): pa[idx] = (pa[idx] * pb[idx] - x) * k
       const DFr p = fe_mul<FrCfg>(ld_packed(a.epi.pa, idx), ld_packed(a.epi.pb, idx));
-      st_packed(a.epi.pa, idx, fe_mul<FrCfg>(fe_sub<FrCfg, 2>(p, x), ld_limbs(a.epi.k, 0)));
+      st_packed(a.epi.pa, idx, fe_mul<FrCfg>(fe_sub<FrCfg, 32>(p, x), ld_limbs(a.epi.k, 0)));
     } else if (a.epi.kind == NttEpilogue::SCALARS) {  // canonical scalar at the natural index
       if (nat < a.epi.n_out) {
         DFr one = fe_zero<FrCfg>();
@@ -140,6 +219,12 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
         q[1] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
       }
     } else {
+      if (!DIF && !a.post_hi) {  // a lazily reduced DIT value (< 22r) -> < 2r for the packed form
+        x = fe_csub<FrCfg, 16>(x);
+        x = fe_csub<FrCfg, 8>(x);
+        x = fe_csub<FrCfg, 4>(x);
+        x = fe_csub<FrCfg, 2>(x);
+      }
       st_packed(data, idx, x);
     }
   }
