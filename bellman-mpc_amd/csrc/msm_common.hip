@@ -241,8 +241,11 @@ MsmShape msm_shape(size_t n, int c_override) {
 }
 
 // With a window table every digit window adds into one shared set of 2^(c-1) buckets, so
-// the accumulation costs n*ceil(256/c) mixed additions and the reduction ~3.6 * 2^(c-1)
-// mixed-addition equivalents (msm_back: ~2.6 full additions per bucket at L = 16), independent of W.
+// the accumulation costs n*ceil(256/c) mixed additions and the reduction ~6.5 * 2^(c-1)
+// mixed-addition equivalents, independent of W.  The reduction does ~3 full additions per bucket
+// (msm_back), but beside the accumulations its latency-bound waves cost about twice their
+// instructions: measured at 2^20 points, c = 16 beats c = 20 by 0.5 ms per proof (a weight of
+// 3.6 picked c = 20 there); c = 20 stays the choice at 2^22.
 // Only window sizes whose top window holds >= 10 real scalar bits: with shared buckets a
 // nearly empty top window (e.g. c = 17: the 16th window only takes the carry; c = 18: 3 bits)
 // pours up to n/2 entries into a handful of small-digit buckets, whose continuation partials
@@ -269,7 +272,7 @@ int msm_table_c(size_t n) {
   for (int c = 8; c <= 24; c++) {
     const int W = (256 + c - 1) / c;
     if (255 - (W - 1) * c < 10) continue;
-    const double cost = (double)n * W + 3.6 * (double)((size_t)1 << (c - 1));
+    const double cost = (double)n * W + 6.5 * (double)((size_t)1 << (c - 1));
     if (cost < best_cost) { best_cost = cost; best = c; }
   }
   return best;

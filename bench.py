@@ -68,6 +68,29 @@ def cpu_model():
     return None
 
 
+def cpu_topology():
+    """physical cores and sockets from /proc/cpuinfo (hardware threads are not cores)"""
+    cores, sockets, phys, core = set(), set(), None, None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "physical id":
+                    phys = v
+                    sockets.add(v)
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None and core is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    if phys is not None and core is not None:
+        cores.add((phys, core))
+    return len(cores) or None, len(sockets) or None
+
+
 def cpu_baseline(bh, ctx, log_c, log_c_1t):
     """bench leg only: the oracle's C++ port of bellman's multicore prover core
     (oracle/cpu/bellman_port.cpp), timed on this host's cores on a bounded sample
@@ -83,14 +106,23 @@ def cpu_baseline(bh, ctx, log_c, log_c_1t):
     proof, ms, ms_syn = cpu_port.chain_prove(params.write(), rounds, threads=threads, reps=reps)
     wall = time.time() - t0
     n_c = 2 * rounds + 2
+    phys, sockets = cpu_topology()
     out = {"value": round(n_c / (ms / 1e3), 1), "unit": "constraints/s", "cores": threads, "kind": "port",
-           "cpu_model": cpu_model(),
+           "threads_are": "hardware threads used (SMT siblings included)", "physical_cores": phys,
+           "sockets": sockets, "cpu_model": cpu_model(),
            "sample": f"median of {reps} prover-core runs (assignment -> proof) of a 2^{log_c}-constraint "
                      f"MiMC chain; bellman's multicore algorithm restated in C++ (oracle/cpu); "
                      f"{wall:.1f} s CPU wall incl. synthesis",
            "ms_per_proof": round(ms, 1), "synthesis_ms": round(ms_syn, 1),
            "end_to_end_value": round(n_c / ((ms + ms_syn) / 1e3), 1),
            "proof_matches_gpu": proof == gpu_proof}
+    full = os.path.join(ROOT, "profiles", "r02_cpu_baseline_2p22.json")
+    if os.path.exists(full):  # the same port once at the headline size (tools/cpu_baseline_full.py)
+        with open(full) as f:
+            fr = json.loads(f.read().strip().splitlines()[-1])
+        out["headline_size_run"] = {k: fr.get(k) for k in ("log_constraints", "value", "ms_per_proof", "threads",
+                                                            "physical_cores", "sockets", "proof_matches_gpu")}
+        out["headline_size_run"]["source"] = "profiles/r02_cpu_baseline_2p22.json (a committed earlier run)"
     if log_c_1t:
         r1 = (1 << (log_c_1t - 1)) - 1
         p1 = bh.Parameters.chain(ctx, r1)
