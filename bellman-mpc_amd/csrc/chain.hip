@@ -7,8 +7,14 @@
 //     asserts) with device fixed-base scalar multiplication (crs.hip).
 // Constants / preimage come from splitmix64 (seed, seed+1) exactly as
 // oracle/circuits.py:fr_stream, so proofs are comparable with the oracle.
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
+#include <functional>
+#include <memory>
+#include <thread>
 #include <vector>
 
 #include "api_internal.h"
@@ -249,6 +255,115 @@ bh_status fixed_base_to_srs(bh_ctx* ctx, const std::vector<AffinePt<T>>& table, 
 
 }  // namespace
 
+// ---------------------------------------------------------------- fused chain synthesis
+// MiMCDemo::synthesize (mimc_mod.rs:50-129) fused with the ProvingAssignment it feeds
+// (prover.rs:55-156) for this circuit: only the recurrence xl' = (xl + c)^3 + xr is serial (the
+// witness); every assignment, linear-combination value and density bit is a function of it, so
+// after the serial pass the rows are written by several threads.  The output is byte-identical
+// to the generic mirror above (the same canonical Montgomery values: add/sub/mul all reduce
+// fully), which BH_CHAIN_GENERIC=1 selects (tests/test_chain_synthesis.py compares the two).
+//   aux:    [xl0, xr0, tmp_0, xl_1, tmp_1, xl_2, ..., tmp_{R-1}]        (2R + 1)
+//   inputs: [one, xl_R]                                                    (2)
+//   row 2i:   a = b = t_i = xl_i + c_i,  c = tmp_i = t_i^2                 (A = xl + one*c_i, C = tmp)
+//   row 2i+1: a = tmp_i,  b = t_i,  c = xl_{i+1} - xr_i                    (A = tmp, C = new_xl - xr)
+//   rows 2R, 2R+1: a = inputs[j], b = c = 0                                (prover.rs:198-204)
+//   a_aux density: every aux but xr0; b_aux: xl0 and xl_1..xl_{R-1}; b_input: one
+struct ChainRows {
+  Fr* a; Fr* b; Fr* c; Fr* inputs; Fr* aux;
+  uint64_t* a_aux_d; uint64_t* b_in_d; uint64_t* b_aux_d;
+};
+
+static bool chain_generic() {
+  static const bool v = [] {
+    const char* e = getenv("BH_CHAIN_GENERIC");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static void parallel_for(size_t n, const std::function<void(size_t, size_t)>& body) {
+  const unsigned hc = std::thread::hardware_concurrency();
+  const size_t T = std::max<size_t>(1, std::min<size_t>({(size_t)(hc ? hc : 1), (size_t)16, n / 65536 + 1}));
+  if (T == 1) { body(0, n); return; }
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < T; k++) th.emplace_back([&, k] { body(n * k / T, n * (k + 1) / T); });
+  for (auto& t : th) t.join();
+}
+
+// fr_stream (same values) with the splitmix64 stream seeked per element -- the state after k
+// draws is seed + k * 0x9E3779B97F4A7C15 -- so the constants are drawn by several threads
+static std::vector<Fr> fr_stream_par(uint64_t seed, size_t count) {
+  std::vector<Fr> out(count);
+  parallel_for(count, [&](size_t lo, size_t hi) {
+    uint64_t st = seed + (uint64_t)(4 * lo) * 0x9E3779B97F4A7C15ull;
+    for (size_t i = lo; i < hi; i++) {
+      uint64_t w[4];
+      for (int k = 0; k < 4; k++) w[k] = splitmix64(st);
+      while (geq_p<4>(w)) sub_p<4>(w);
+      out[i] = fr_from_canonical(w);
+    }
+  });
+  return out;
+}
+
+static void chain_fused(size_t R, uint64_t seed, uint64_t preimage_seed, const ChainRows& o) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::vector<Fr> consts = fr_stream_par(seed, R);
+  const std::vector<Fr> pre = fr_stream(preimage_seed, 2);
+  const auto t1 = std::chrono::steady_clock::now();
+  // serial pass: the witness.  xl[i] for i <= R, t and tmp per round (aux holds tmp/xl in place)
+  // uninitialised (Fr is trivially constructible): the pages are first touched by the writers
+  std::unique_ptr<Fr[]> xl(new Fr[R + 1]), t(new Fr[R]);
+  xl[0] = pre[0];
+  Fr xr = pre[1];
+  for (size_t i = 0; i < R; i++) {
+    t[i] = add(xl[i], consts[i]);
+    const Fr tmp = sqr(t[i]);
+    o.aux[2 + 2 * i] = tmp;
+    xl[i + 1] = add(mul(t[i], tmp), xr);
+    xr = xl[i];
+  }
+  const auto t2 = std::chrono::steady_clock::now();
+  if (getenv("BH_HOST_TIMING"))
+    fprintf(stderr, "chain synthesis: constants %.1f ms, recurrence %.1f ms\n",
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count());
+  // rows, assignments and densities in parallel
+  const size_t na = 2 * R + 1, nw = (na + 63) / 64;
+  o.aux[0] = pre[0];
+  o.aux[1] = pre[1];
+  o.inputs[0] = Fr::one();
+  o.inputs[1] = xl[R];
+  parallel_for(R, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) {
+      const Fr& tmp = o.aux[2 + 2 * i];
+      if (i + 1 < R) o.aux[3 + 2 * i] = xl[i + 1];
+      const Fr& xri = i ? xl[i - 1] : pre[1];
+      o.a[2 * i] = t[i]; o.b[2 * i] = t[i]; o.c[2 * i] = tmp;
+      o.a[2 * i + 1] = tmp; o.b[2 * i + 1] = t[i]; o.c[2 * i + 1] = sub(xl[i + 1], xri);
+    }
+  });
+  for (int j = 0; j < 2; j++) {
+    o.a[2 * R + j] = o.inputs[j];
+    o.b[2 * R + j] = Fr::zero();
+    o.c[2 * R + j] = Fr::zero();
+  }
+  parallel_for(nw, [&](size_t lo, size_t hi) {
+    for (size_t w = lo; w < hi; w++) {
+      uint64_t am = ~0ull, bm = 0;
+      for (int k = 0; k < 64; k++) {
+        const size_t idx = w * 64 + (size_t)k;
+        if (idx >= na) { am &= ~(1ull << k); continue; }
+        if (idx == 1) am &= ~(1ull << k);                                   // xr0 is in no A
+        if (idx == 0 || ((idx & 1) && idx >= 3)) bm |= 1ull << k;           // xl0, xl_1..xl_{R-1}
+      }
+      o.a_aux_d[w] = am;
+      o.b_aux_d[w] = bm;
+    }
+  });
+  o.b_in_d[0] = 1;  // one appears in every B
+}
+
 extern "C" {
 
 bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness** out) {
@@ -258,6 +373,25 @@ bh_status bh_chain_witness(bh_ctx* ctx, size_t rounds, uint64_t seed, bh_witness
 bh_status bh_chain_witness_preimage(bh_ctx* ctx, size_t rounds, uint64_t seed, uint64_t preimage_seed,
                                     bh_witness** out) {
   if (!ctx || !out || rounds == 0) return BH_ERR_INVALID_ARGUMENT;
+  if (!chain_generic()) {
+    const size_t nc = 2 * rounds + 2, na = 2 * rounds + 1, nw = (na + 63) / 64;
+    std::unique_ptr<Fr[]> a(new Fr[nc]), b(new Fr[nc]), c(new Fr[nc]), in(new Fr[2]), aux(new Fr[na]);
+    std::vector<uint64_t> ad(nw), bd(nw), bi(1);
+    const auto t0 = std::chrono::steady_clock::now();
+    chain_fused(rounds, seed, preimage_seed, ChainRows{a.get(), b.get(), c.get(), in.get(), aux.get(),
+                                                       ad.data(), bi.data(), bd.data()});
+    const auto t1 = std::chrono::steady_clock::now();
+    const bh_status st = bh_witness_upload(ctx, a[0].v, b[0].v, c[0].v, nc, in[0].v, 2, aux[0].v, na, ad.data(),
+                                           bi.data(), bd.data(), out);
+    if (getenv("BH_HOST_TIMING")) {
+      auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+        return std::chrono::duration<double, std::milli>(y - x).count();
+      };
+      fprintf(stderr, "chain witness: synthesis %.1f ms, upload %.1f ms\n", ms(t0, t1),
+              ms(t1, std::chrono::steady_clock::now()));
+    }
+    return st;
+  }
   const std::vector<Fr> consts = fr_stream(seed, rounds);
   const std::vector<Fr> pre = fr_stream(preimage_seed, 2);
   ProvingAssignmentN cs;
@@ -288,6 +422,14 @@ bh_status bh_chain_assignment(size_t rounds, uint64_t seed, uint64_t preimage_se
   if (st) return st;
   if (!a || !b || !c || !inputs || !aux || !a_aux_density || !b_input_density || !b_aux_density)
     return BH_ERR_INVALID_ARGUMENT;
+  if (!chain_generic()) {
+    static_assert(sizeof(Fr) == 32, "Fr layout");
+    chain_fused(rounds, seed, preimage_seed,
+                ChainRows{reinterpret_cast<Fr*>(a), reinterpret_cast<Fr*>(b), reinterpret_cast<Fr*>(c),
+                          reinterpret_cast<Fr*>(inputs), reinterpret_cast<Fr*>(aux), a_aux_density,
+                          b_input_density, b_aux_density});
+    return BH_OK;
+  }
   const std::vector<Fr> consts = fr_stream(seed, rounds);
   const std::vector<Fr> pre = fr_stream(preimage_seed, 2);
   ProvingAssignmentN cs;

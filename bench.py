@@ -348,7 +348,7 @@ def main():
         "roofline": roof,
         "valu_roofline": valu,
         "end_to_end": {"value": round(n_constraints / (t_wit + ms / 1e3), 1), "unit": "constraints/s",
-                       "note": "host witness synthesis (single thread, native) + upload + prover core"},
+                       "note": "host witness synthesis (native; serial MiMC recurrence, rows/densities/constants on several threads) + upload + prover core"},
         "cpu_baseline": base,
         "breakdown_ms": {"h_pipeline": round(sum(t[1] for t in timings) / len(timings), 3),
                          "g1_accumulate": round(acc_ms / len(timings), 3),
