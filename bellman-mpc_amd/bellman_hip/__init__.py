@@ -72,6 +72,8 @@ def _load():
     sig = {
         "bh_status_string": (ctypes.c_char_p, [I]),
         "bh_version": (I, []),
+        "bh_verify_proof": (I, [P, S, P, P, S, P]),
+        "bh_verify_batch": (I, [P, S, P, P, S, S, P, P]),
         "bh_ctx_create": (I, [I, P]),
         "bh_ctx_destroy": (I, [P]),
         "bh_ctx_reserve": (I, [P, S, U8]),
@@ -152,7 +154,7 @@ EXPORTED_SYMBOLS = [
     "bh_chain_witness_preimage", "bh_prove_witness_partial_comm", "bh_prove_witness_partials_local",
     "bh_comm_allgather", "bh_comm_allreduce_max", "bh_comm_info", "bh_params_prepare_shard", "bh_last_stats",
     "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
-    "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch",
+    "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch", "bh_verify_proof", "bh_verify_batch",
 ]
 PARTIAL_BYTES = 960
 
@@ -739,6 +741,36 @@ def proof_from_partials(vk_bytes, partials, nshards, r, s):
     _check(_lib.bh_proof_from_partials(_ptr(vk), vk.size, _ptr(parts), nshards, _ptr(rr), _ptr(ss), _ptr(out)),
            "proof_from_partials")
     return out.tobytes()
+
+
+def verify_proof(vk_bytes, proof, public_inputs):
+    """verify_proof (verifier.rs:11-62) on the host: vk = VerifyingKey::write bytes (or the
+    head of Parameters::write), proof = Proof::write bytes, public_inputs = ints without ONE.
+    Raises on malformed data (e.g. the wrong number of inputs); returns bool."""
+    vk = np.frombuffer(bytes(vk_bytes), dtype=np.uint8)
+    pf = np.frombuffer(bytes(proof), dtype=np.uint8)
+    assert pf.size == 192
+    ins = fr_to_canonical_limbs(public_inputs) if public_inputs else np.zeros((1, 4), dtype=np.uint64)
+    ok = ctypes.c_int()
+    _check(_lib.bh_verify_proof(_ptr(vk), vk.size, _ptr(pf), _ptr(ins), len(public_inputs), ctypes.byref(ok)),
+           "verify_proof")
+    return bool(ok.value)
+
+
+def verify_batch(vk_bytes, proofs, public_inputs, zs):
+    """Batch verifier (verifier/batch.rs:95-169): proofs = list of 192-byte proofs,
+    public_inputs = list (one per proof) of input lists, zs = the random nonzero scalars."""
+    k = len(proofs)
+    vk = np.frombuffer(bytes(vk_bytes), dtype=np.uint8)
+    pf = np.frombuffer(b"".join(bytes(p) for p in proofs) or b"\0", dtype=np.uint8)
+    ni = len(public_inputs[0]) if k else 0
+    flat = [x for row in public_inputs for x in row]
+    ins = fr_to_canonical_limbs(flat) if flat else np.zeros((1, 4), dtype=np.uint64)
+    z = fr_to_canonical_limbs(zs) if zs else np.zeros((1, 4), dtype=np.uint64)
+    ok = ctypes.c_int()
+    _check(_lib.bh_verify_batch(_ptr(vk), vk.size, _ptr(pf), _ptr(ins), ni, k, _ptr(z), ctypes.byref(ok)),
+           "verify_batch")
+    return bool(ok.value)
 
 
 def device_count():

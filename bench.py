@@ -321,6 +321,12 @@ def main():
         dropin = {"value": round(n_constraints / (dms / 1e3), 1), "unit": "constraints/s", "ms_per_step": round(dms, 3),
                   "witness_bytes": wbytes, "proof_matches": pd == p0 == ref,
                   "note": "bh_prove from host (pageable) buffers: witness upload overlapped with the proof"}
+        # the proof is valid: the native verifier (verify_proof, verifier.rs:23-62) on the public
+        # input (the chain's image; input 0 is ONE)
+        public = bh.fr_from_mont(asg["inputs"])[1:]
+        t0 = time.perf_counter()
+        dropin["proof_verifies"] = bh.verify_proof(vk, ref, public)
+        dropin["verify_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         del asg
     # CPU baseline: rank 0 of a 1-GPU run only (a bounded sample; see cpu_baseline)
     base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints)

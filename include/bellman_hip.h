@@ -183,6 +183,19 @@ bh_status bh_shard_range(size_t n, size_t shard, size_t nshards, size_t* lo, siz
 bh_status bh_prove_witness_partial(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard,
                                    size_t nshards, uint8_t partial_out[960]);
 bh_status bh_vk_write(const bh_params* p, uint8_t* out, size_t cap, size_t* written);
+
+/* ---- verification (host only, no device needed): verify_proof (verifier.rs:11-62) and the batch
+ * verifier (verifier/batch.rs:95-169) over a BLS12-381 pairing.  vk: VerifyingKey::write bytes (the
+ * head of Parameters::write, or bh_vk_write); proof: Proof::write bytes (192, decoded like Proof::read:
+ * compressed, torsion-checked, identity rejected); public inputs: num_inputs canonical Fr, 4 LE u64
+ * each, without the implicit ONE.  *valid = 1 iff the proof(s) verify; the status is non-zero only for
+ * malformed data (num_inputs + 1 != ic length: BH_ERR_INVALID_ARGUMENT, the reference's
+ * VerificationError::InvalidVerifyingKey).  Batch: k proofs, inputs k * num_inputs * 4 words, and the
+ * caller's random nonzero scalars z (k * 4 canonical words; the reference draws them from a CryptoRng). */
+bh_status bh_verify_proof(const uint8_t* vk, size_t vk_len, const uint8_t* proof, const uint64_t* inputs,
+                          size_t num_inputs, int* valid);
+bh_status bh_verify_batch(const uint8_t* vk, size_t vk_len, const uint8_t* proofs, const uint64_t* inputs,
+                          size_t num_inputs, size_t k, const uint64_t* z, int* valid);
 bh_status bh_proof_from_partials(const uint8_t* vk_bytes, size_t vk_len, const uint8_t* partials, size_t nshards,
                                  const uint64_t r[4], const uint64_t s[4], uint8_t proof_out[192]);
 

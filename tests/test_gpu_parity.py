@@ -634,3 +634,23 @@ def test_g2_msm_2p16_equals_cpu_port(ctx, dense):
     got = bh.multiexp(ctx, bases, off, None if bits is None else list(bits), ex)
     want, _ = cpu_port.multiexp(2, b_g2, ex, off, words, threads=16)
     assert got == want
+
+
+def test_c5_batch_proofs_pass_the_native_batch_verifier(ctx):
+    """Throughput-mode proofs (distinct preimages, shared Parameters) accepted by the native
+    batch verifier (verifier/batch.rs:95-169) and each by verify_proof; one tampered proof
+    makes the batch fail."""
+    bh = _bh()
+    rounds = (1 << 11) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    ws = [bh.Witness.chain(ctx, rounds, seed=7, preimage_seed=20 + i) for i in range(4)]
+    proofs = bh.prove_batch(ctx, params, ws, 27134, 17146)
+    vk = params.vk_bytes()
+    publics = [bh.fr_from_mont(bh.chain_assignment(rounds, seed=7, preimage_seed=20 + i)["inputs"])[1:]
+               for i in range(4)]
+    for p, pub in zip(proofs, publics):
+        assert bh.verify_proof(vk, p, pub)
+    rng = random.Random(5)
+    zs = [rng.randrange(1, R) for _ in proofs]
+    assert bh.verify_batch(vk, proofs, publics, zs)
+    assert not bh.verify_batch(vk, proofs, publics[1:] + publics[:1], zs)
