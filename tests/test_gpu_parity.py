@@ -654,3 +654,54 @@ def test_c5_batch_proofs_pass_the_native_batch_verifier(ctx):
     zs = [rng.randrange(1, R) for _ in proofs]
     assert bh.verify_batch(vk, proofs, publics, zs)
     assert not bh.verify_batch(vk, proofs, publics[1:] + publics[:1], zs)
+
+
+@pytest.mark.parametrize("value", [0, 1, 5, R - 1])
+def test_degenerate_scalars_tables_plain_and_shards_agree(ctx, value):
+    """Edge scalars at prover size (2^17 constraints, window tables in use): every aux scalar
+    equal (0: every multiexp empty; 1 and 5: all entries of a window in one bucket, whose
+    continuation partials span every segment -- the log-depth fix-up path; r-1: every signed
+    digit at its extreme with carries).  Not a satisfying assignment, so the proof is not
+    valid, but tables vs plain windows vs two shards compute the same multiexps byte for byte."""
+    bh = _bh()
+    rounds = (1 << 16) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    asg["aux"][:] = bh.fr_to_mont([value])[0]
+    h = bh.ctypes.c_void_p()
+    bh._check(bh._lib.bh_witness_upload(ctx.h, bh._ptr(asg["a"]), bh._ptr(asg["b"]), bh._ptr(asg["c"]),
+                                        asg["a"].shape[0], bh._ptr(asg["inputs"]), asg["inputs"].shape[0],
+                                        bh._ptr(asg["aux"]), asg["aux"].shape[0], bh._ptr(asg["a_aux_density"]),
+                                        bh._ptr(asg["b_input_density"]), bh._ptr(asg["b_aux_density"]),
+                                        bh.ctypes.byref(h)), "bh_witness_upload")
+    w = bh.Witness(ctx, h, asg["a"].shape[0])
+    ctx.set_tables(False)
+    try:
+        plain = bh.prove_witness(ctx, params, w, 27134, 17146)
+    finally:
+        ctx.set_tables(True)
+    params.prepare(w)
+    assert bh.prove_witness(ctx, params, w, 27134, 17146) == plain
+    parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, 2) for k in range(2))
+    assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
+
+
+def test_msm_empty_and_single(ctx, golden):
+    """Empty exponent list -> identity (multiexp.rs: the fold over no windows is zero); one
+    exponent -> that multiple of the first base (against the oracle), both groups, sync and
+    async seams."""
+    from oracle import bls12_381 as bls
+    bh = _bh()
+    for group, data in ((bh.BH_G1, golden["msm_g1"]), (bh.BH_G2, golden["msm_g2"])):
+        bases = _bases(ctx, group, data["bases"])
+        ident = bytes([0x40]) + bytes((96 if group == bh.BH_G1 else 192) - 1)
+        assert bh.multiexp(ctx, bases, 0, None, []) == ident
+        assert bh.multiexp_async(ctx, bases, 0, None, []).wait() == ident
+        k = 0x1234567890ABCDEF1234567890ABCDEF
+        got = bh.multiexp(ctx, bases, 0, None, [k])
+        G = bls.G1 if group == bh.BH_G1 else bls.G2
+        base = (bls.g1_from_uncompressed if group == bh.BH_G1 else bls.g2_from_uncompressed)(
+            bytes.fromhex(data["bases"][0]), checked=False)[1]
+        want = G.to_affine(G.mul(G.from_affine(base), k))
+        enc = bls.g1_to_uncompressed if group == bh.BH_G1 else bls.g2_to_uncompressed
+        assert got == enc(want)

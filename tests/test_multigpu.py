@@ -95,3 +95,57 @@ def test_bench_gpus_more_than_devices_fails_loudly():
                         "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert "devices" in p.stderr
+
+
+def _gloo_rank(rank, world, port, rounds, q):
+    sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
+    import torch
+    import torch.distributed as dist
+    import bellman_hip as bh
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = bh.Context(0)
+    try:
+        params = bh.Parameters.chain(ctx, rounds)
+        w = bh.Witness.chain(ctx, rounds)
+        rec = bh.prove_witness_partial(ctx, params, w, rank, world)
+        t = torch.frombuffer(bytearray(rec), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        if rank == 0:
+            parts = b"".join(x.numpy().tobytes() for x in out)
+            proof = bh.proof_from_partials(params.vk_bytes(), parts, world, R, S)
+            q.put(proof == bh.prove_witness(ctx, params, w, R, S))
+        dist.barrier()
+    finally:
+        ctx.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,logc", [(2, 12), (3, 16)])
+def test_rank_processes_exchange_partials_over_gloo(world, logc):
+    """The product's per-rank path in separate processes (one context each, as bench.py's
+    ranks run), partial records exchanged by a real collective (gloo all-gather, standing in
+    for the ncclAllGather of bh_prove_witness_partial_comm), recombined by rank 0: equal to the
+    single-device proof.  Ranks share cuda:0 here; 2-3 processes on the card."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mctx = mp.get_context("spawn")
+    q = mctx.Queue()
+    procs = [mctx.Process(target=_gloo_rank, args=(r, world, port, (1 << (logc - 1)) - 1, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        ok = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert ok
+    assert all(p.exitcode == 0 for p in procs)
