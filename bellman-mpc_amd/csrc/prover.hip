@@ -1014,9 +1014,15 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ctx->last_timings[9] = (double)g2_adds;
   ctx->last_timings[10] = n_table;
   ctx->last_timings[11] = n_large;
-  size_t tb = params->h.win.bytes + params->l.win.bytes + params->a.win.bytes + params->b_g1.win.bytes +
-              params->b_g2.win.bytes;
-  for (const auto& kv : params->h_shares) tb += kv.second->win.bytes;
+  // bytes of the window tables this proof's multiexps read (each distinct table once): for a
+  // shard, its own slices and h share only, not whatever else the Parameters keep resident
+  size_t tb = 0;
+  for (int j = 0; j < 8; j++) {
+    if (!use_table[j]) continue;
+    bool seen = false;
+    for (int q = 0; q < j; q++) seen |= use_table[q] && jobs[q].srs == jobs[j].srs;
+    if (!seen) tb += jobs[j].srs->win.bytes;
+  }
   ctx->last_timings[12] = (double)tb;
   drain.ok = true;
   return BH_OK;

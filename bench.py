@@ -262,11 +262,15 @@ def main():
             timings.append(ctx.last_timings())
     barrier()
     elapsed = time.perf_counter() - t_start
+    # window tables the timed proofs read (rank 0 of N, or every rank's own slices for N > 1)
+    st = ctx.last_stats()
+    tables = {"used": int(st[10]), "large_multiexps": int(st[11]), "GB": round(st[12] / 1e9, 2)}
     per_rank_ms = None
     if comm is not None:
-        mine = elapsed * 1000.0 / args.steps
-        per_rank_ms = [round(json.loads(x.decode().strip()), 3)
-                       for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(32))]
+        mine = [elapsed * 1000.0 / args.steps, tables["used"], tables["large_multiexps"], tables["GB"]]
+        recs = [json.loads(x.decode().strip()) for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(96))]
+        per_rank_ms = [round(x[0], 3) for x in recs]
+        tables = {"used": [x[1] for x in recs], "large_multiexps": [x[2] for x in recs], "GB": [x[3] for x in recs]}
         elapsed = comm.allreduce_max(elapsed)
     ms = elapsed * 1000.0 / args.steps
     value = n_constraints * args.steps / elapsed
@@ -349,6 +353,7 @@ def main():
                    "exchange": "rccl" if world > 1 else None},
         "rccl": rccl,
         "per_rank_ms_per_step": per_rank_ms,
+        "srs_window_tables": tables,
         "dropin": dropin,
         "c5": c5,
         "roofline": roof,

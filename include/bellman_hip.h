@@ -268,8 +268,9 @@ bh_status bh_params_write(const bh_params* p, uint8_t* out, size_t cap, size_t* 
  * [6] G2 launches, [7] G2 pairs, [8] G1 mixed additions, [9] G2 mixed additions */
 bh_status bh_last_timings(const bh_ctx* ctx, double out[10]);
 /* bh_last_timings' fields followed by [10] large multiexps that used a window table,
- * [11] large multiexps (those a table would serve), [12] window-table bytes resident for the
- * Parameters; n entries are written (missing ones 0). */
+ * [11] large multiexps (those a table would serve), [12] bytes of the window tables the proof
+ * read (each distinct table once: for a shard, its own slices); n entries are written (missing
+ * ones 0). */
 bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
 
 #ifdef __cplusplus
