@@ -965,20 +965,22 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   for (int q = 0; q < nbig; q++)
     if ((s = tail_job(big[q], tails[q]))) return s;
   const auto t_enq = std::chrono::steady_clock::now();
-  BH_TRY_HIP(hipStreamSynchronize(sS));
-  BH_TRY_HIP(hipStreamSynchronize(sA));
-  BH_TRY_HIP(hipStreamSynchronize(sH));
-  BH_TRY_HIP(hipStreamSynchronize(sT));
-  for (int q = 0; q < nbig; q++) BH_TRY_HIP(hipStreamSynchronize(tails[q]));
-  const auto t_gpu = std::chrono::steady_clock::now();
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0, g1_adds = 0, g2_adds = 0;
   int g1_launches = 0, g2_launches = 0;
   for (int i = 0; i < 6; i++) res1[i] = jac_identity<Fp>();
   for (int i = 0; i < 2; i++) res2[i] = jac_identity<bh::Fp2>();
-  for (int j = 0; j < 8; j++) {
+  // Each multiexp's host combine runs as soon as its own tail stream is done (its window sums
+  // are on the host), while later tails still run: only the last one's stays on the critical
+  // path.  The small multiexps (stream sT) finish first.
+  int order[8], nord = 0;
+  for (int i = 0; i < nsmall; i++) order[nord++] = small[i];
+  for (int q = 0; q < nbig; q++) order[nord++] = big[q];
+  for (int o = 0; o < nord; o++) {
+    const int j = order[o];
     const Job& J = jobs[j];
-    if (his[j] == los[j]) continue;
+    if (o == 0 || o == nsmall) BH_TRY_HIP(hipStreamSynchronize(sT));
+    if (o >= nsmall) BH_TRY_HIP(hipStreamSynchronize(tails[o - nsmall]));
     float t = 0;
     if (acc_events_on()) (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
     const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
@@ -990,6 +992,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       g1_acc_ms += t; g1_launches++; g1_pairs += pairs; g1_adds += ctx->host_counts[j];
     }
   }
+  BH_TRY_HIP(hipStreamSynchronize(sS));
+  BH_TRY_HIP(hipStreamSynchronize(sA));
+  BH_TRY_HIP(hipStreamSynchronize(sH));
+  BH_TRY_HIP(hipStreamSynchronize(sT));
+  const auto t_gpu = std::chrono::steady_clock::now();
 
   const auto t1 = std::chrono::steady_clock::now();
   static const bool host_timing = getenv("BH_HOST_TIMING") != nullptr;
@@ -997,7 +1004,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, enqueue done %.3f, gpu done %.3f, combine %.3f\n",
+    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, enqueue done %.3f, gpu and combines done %.3f, after %.3f\n",
             ms(t0, t_acc0), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
   }
   float h_ms = 0;
@@ -1029,28 +1036,42 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
 }
 
 // proof assembly (prover.rs:315-349) -> Proof::write (groth16/mod.rs:42-48)
-void assemble(const VkHost& vk, const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], const uint64_t r_in[4],
-              const uint64_t s_in[4], uint8_t proof_out[192]) {
+// The terms of A, B and C that depend only on the verifying key and r, s (5 of the 7 scalar
+// multiplications): computed on a host thread while the device works.
+struct AssemblePre {
+  uint64_t rc[4], sc[4];
+  Jac<Fp> g_a, g_c;
+  Jac<bh::Fp2> g_b;
+};
+
+AssemblePre assemble_pre(const VkHost& vk, const uint64_t r_in[4], const uint64_t s_in[4]) {
+  AssemblePre p;
   Fr r = fr_from_canonical(r_in), sv = fr_from_canonical(s_in);
-  uint64_t rc[4], sc[4], rsc[4];
-  fr_to_canonical(r, rc);
-  fr_to_canonical(sv, sc);
+  uint64_t rsc[4];
+  fr_to_canonical(r, p.rc);
+  fr_to_canonical(sv, p.sc);
   fr_to_canonical(mul(r, sv), rsc);
   const Jac<Fp> d1 = jac_from_affine(vk.delta_g1);
   const Jac<bh::Fp2> d2 = jac_from_affine(vk.delta_g2);
-  Jac<Fp> g_a = jac_add(jac_mul(d1, rc, 4), jac_from_affine(vk.alpha_g1));
-  Jac<bh::Fp2> g_b = jac_add(jac_mul(d2, sc, 4), jac_from_affine(vk.beta_g2));
-  Jac<Fp> g_c = jac_mul(d1, rsc, 4);
-  g_c = jac_add(g_c, jac_mul(jac_from_affine(vk.alpha_g1), sc, 4));
-  g_c = jac_add(g_c, jac_mul(jac_from_affine(vk.beta_g1), rc, 4));
+  p.g_a = jac_add(jac_mul(d1, p.rc, 4), jac_from_affine(vk.alpha_g1));
+  p.g_b = jac_add(jac_mul(d2, p.sc, 4), jac_from_affine(vk.beta_g2));
+  p.g_c = jac_mul(d1, rsc, 4);
+  p.g_c = jac_add(p.g_c, jac_mul(jac_from_affine(vk.alpha_g1), p.sc, 4));
+  p.g_c = jac_add(p.g_c, jac_mul(jac_from_affine(vk.beta_g1), p.rc, 4));
+  return p;
+}
+
+void assemble_finish(const AssemblePre& p, const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], uint8_t proof_out[192]) {
+  Jac<Fp> g_a = p.g_a, g_c = p.g_c;
+  Jac<bh::Fp2> g_b = p.g_b;
   Jac<Fp> a_answer = jac_add(r1[2], r1[3]);
   g_a = jac_add(g_a, a_answer);
-  a_answer = jac_mul(a_answer, sc, 4);
+  a_answer = jac_mul(a_answer, p.sc, 4);
   g_c = jac_add(g_c, a_answer);
   Jac<Fp> b1_answer = jac_add(r1[4], r1[5]);
   Jac<bh::Fp2> b2_answer = jac_add(r2[0], r2[1]);
   g_b = jac_add(g_b, b2_answer);
-  b1_answer = jac_mul(b1_answer, rc, 4);
+  b1_answer = jac_mul(b1_answer, p.rc, 4);
   g_c = jac_add(g_c, b1_answer);
   g_c = jac_add(g_c, r1[0]);
   g_c = jac_add(g_c, r1[1]);
@@ -1058,6 +1079,36 @@ void assemble(const VkHost& vk, const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], c
   g2_to_compressed(jac_to_affine(g_b), proof_out + 48);
   g1_to_compressed(jac_to_affine(g_c), proof_out + 144);
 }
+
+void assemble(const VkHost& vk, const Jac<Fp> r1[6], const Jac<bh::Fp2> r2[2], const uint64_t r_in[4],
+              const uint64_t s_in[4], uint8_t proof_out[192]) {
+  assemble_finish(assemble_pre(vk, r_in, s_in), r1, r2, proof_out);
+}
+
+// assemble_pre on its own host thread, started before the device work is enqueued (~0.1 ms of
+// the ~0.2 ms assembly leaves the critical path); computed inline if no thread can be started.
+struct AssemblePreThread {
+  VkHost vk;
+  uint64_t r[4], s[4];
+  AssemblePre pre;
+  std::thread th;
+  AssemblePreThread(const VkHost& v, const uint64_t r_in[4], const uint64_t s_in[4]) : vk(v) {
+    memcpy(r, r_in, sizeof r);
+    memcpy(s, s_in, sizeof s);
+    try {
+      th = std::thread([this] { pre = assemble_pre(vk, r, s); });
+    } catch (...) {
+      pre = assemble_pre(vk, r, s);
+    }
+  }
+  const AssemblePre& get() {
+    if (th.joinable()) th.join();
+    return pre;
+  }
+  ~AssemblePreThread() {
+    if (th.joinable()) th.join();
+  }
+};
 
 VkHost vk_of(const bh_params* p) {
   return VkHost{p->alpha_g1, p->beta_g1, p->delta_g1, p->beta_g2, p->delta_g2};
@@ -1257,10 +1308,11 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
   BH_TRY_HIP(hipSetDevice(ctx->device));
   Jac<Fp> r1[6];
   Jac<bh::Fp2> r2[2];
+  AssemblePreThread pre(vk_of(params), r_in, s_in);
   bh_status s = compute_msms_sync(ctx, params, w, 0, 1, r1, r2);
   if (s) return s;
   const auto t0 = std::chrono::steady_clock::now();
-  assemble(vk_of(params), r1, r2, r_in, s_in, proof_out);
+  assemble_finish(pre.get(), r1, r2, proof_out);
   const double asm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   ctx->last_timings[0] += asm_ms;
   if (getenv("BH_HOST_TIMING")) fprintf(stderr, "assemble %.3f ms\n", asm_ms);
@@ -1367,13 +1419,14 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
     // (same-box A/B at 2^20: 19.7 ms per proof with one lane, 19.8 with two, 21.6 with three),
     // and every extra context adds 13 streams, i.e. hardware queues: beyond the 16 the library
     // asks for, queues time-share and a proof takes ~33 ms.
-    const VkHost vk1 = vk_of(params);
+    // r and s are shared by the batch: their terms of A, B, C once, beside the first proof
+    AssemblePreThread pre(vk_of(params), r_in, s_in);
     for (size_t i = 0; i < k; i++) {
       Jac<Fp> r1[6];
       Jac<bh::Fp2> r2[2];
       bh_status st1 = compute_msms_sync(ctx, params, ws[i], 0, 1, r1, r2, nullptr, true);
       if (st1) return st1;
-      assemble(vk1, r1, r2, r_in, s_in, proofs_out + 192 * i);
+      assemble_finish(pre.get(), r1, r2, proofs_out + 192 * i);
     }
     return BH_OK;
   }
@@ -1401,7 +1454,7 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
       if (st) return st;
     }
   }
-  const VkHost vk = vk_of(params);
+  const AssemblePre pre = assemble_pre(vk_of(params), r_in, s_in);
   std::vector<bh_status> st(L, BH_OK);
   std::vector<std::thread> th;
   for (int l = 0; l < L; l++)
@@ -1414,7 +1467,7 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
         Jac<bh::Fp2> r2[2];
         st[l] = compute_msms_sync(v, params, ws[i], 0, 1, r1, r2, nullptr, false);
         if (st[l]) return;
-        assemble(vk, r1, r2, r_in, s_in, proofs_out + 192 * i);
+        assemble_finish(pre, r1, r2, proofs_out + 192 * i);
       }
     });
   for (auto& t : th) t.join();
@@ -1525,12 +1578,13 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
   });
   Jac<Fp> r1[6];
   Jac<bh::Fp2> r2[2];
+  AssemblePreThread pre(vk_of(params), r, s);
   st = compute_msms_sync(ctx, params, w, 0, 1, r1, r2, nullptr, true, &up);
   uploader.join();
   (void)hipStreamSynchronize(ctx->h2d);
   if (st) return st;
   if (ust) return ust;
-  assemble(vk_of(params), r1, r2, r, s, proof_out);
+  assemble_finish(pre.get(), r1, r2, proof_out);
   ctx->last_timings[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return BH_OK;
 }
