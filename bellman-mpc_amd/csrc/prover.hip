@@ -948,7 +948,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
   if (nbig > 0) {
-    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + sorder[pre_sorts - 1]], 0));
+    // wait for the last pre-sort that is a real sort: a trailing copy of another multiexp's
+    // entries (b_g1_aux from b_g2_aux) is ~0.15 ms of blits that can run beside the accumulation
+    int wait_j = big[0];
+    for (int r = 0; r < pre_sorts; r++)
+      if (sorted_from[sorder[r]] == sorder[r]) wait_j = sorder[r];
+    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + wait_j], 0));
     if ((s = acc_job(big[0], sA))) return s;
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
