@@ -705,3 +705,39 @@ def test_msm_empty_and_single(ctx, golden):
         want = G.to_affine(G.mul(G.from_affine(base), k))
         enc = bls.g1_to_uncompressed if group == bh.BH_G1 else bls.g2_to_uncompressed
         assert got == enc(want)
+
+
+def test_two_contexts_share_one_parameters(ctx):
+    """The 'shared Parameters' use: one Parameters and one witness, created on
+    the fixture's context and without prepared tables, proved from two other contexts on two
+    host threads at once.  The first proofs race to build the window tables (exclusive lock,
+    synchronised build) while the other reads under the shared lock; every proof equals the
+    single-context one."""
+    import threading
+    bh = _bh()
+    rounds = (1 << 16) - 1  # 2^17 constraints: the large multiexps use window tables
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    ctxs = [bh.Context(0), bh.Context(0)]
+    results, errors = [], []
+
+    def worker(c):
+        try:
+            for _ in range(2):
+                results.append(bh.prove_witness(c, params, w, 27134, 17146))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(repr(e))
+
+    try:
+        threads = [threading.Thread(target=worker, args=(c,)) for c in ctxs]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        assert not errors, errors
+        assert ctxs[0].last_stats()[10] > 0  # the window tables were used
+        single = bh.prove_witness(ctx, params, w, 27134, 17146)
+        assert len(results) == 4 and set(results) == {single}
+    finally:
+        for c in ctxs:
+            c.close()
