@@ -34,6 +34,8 @@ TRAFFIC_FILE = "r02_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py outp
 G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X (profiles/r01_curvebench.txt)
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
+PMC_FILE = "r02_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench
+SOLO_WAVE_INSTR_RATE = 515.0   # G wave-instr/s: the G1 accumulation alone (6.3 G madd/s x 5234 lane-instr / 64)
 
 
 def parse():
@@ -304,6 +306,24 @@ def main():
             "mad_u64_tps": round(madd_rate * MADS_PER_G1_MADD / 1e3, 2) if madd_rate else None,
             "mad_u64_frac": round(madd_rate * MADS_PER_G1_MADD / 1e3 / MAD_U64_PEAK_TPS, 4) if madd_rate else None,
             "mad_u64_peak_tps": MAD_U64_PEAK_TPS, "mad_u64_peak_source": "tools/microbench/madbench.hip"}
+    # whole-proof VALU issue: the PMC pass's VALU wave-instructions per proof (every kernel)
+    # against the rate the G1 accumulation issues at alone
+    proof_valu = None
+    ppath = os.path.join(ROOT, "profiles", PMC_FILE)
+    if os.path.exists(ppath) and k == 22 and world == 1:
+        with open(ppath) as f:
+            pmc = json.load(f)
+        per = [v for v in pmc.values() if isinstance(v, dict) and "SQ_INSTS_VALU" in v]
+        g1 = [v for key, v in pmc.items() if key.startswith("k_accumulate_pf<CurveOps<FpOps>")]
+        if per and g1:
+            n_proofs = g1[0]["dispatches"]["SQ_INSTS_VALU"] / 6  # six G1 multiexps per proof
+            wi = sum(v["SQ_INSTS_VALU"] * v["dispatches"]["SQ_INSTS_VALU"] for v in per) / n_proofs
+            rate = wi / (ms / 1e3) / 1e9
+            proof_valu = {"wave_instructions_per_proof": round(wi), "achieved": round(rate, 1),
+                          "peak": SOLO_WAVE_INSTR_RATE, "unit": "G VALU wave-instructions/s",
+                          "frac": round(rate / SOLO_WAVE_INSTR_RATE, 4),
+                          "source": f"profiles/{PMC_FILE} (SQ_INSTS_VALU, every dispatch) / this run's ms_per_step",
+                          "peak_source": "k_accumulate_pf<G1> alone (BH_PROVER_SERIAL=1): 6.3 G madd/s x 5234 / 64"}
     c5 = c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier) if args.c5 else None
     if rank != 0:
         comm.close()
@@ -358,6 +378,7 @@ def main():
         "c5": c5,
         "roofline": roof,
         "valu_roofline": valu,
+        "proof_valu_issue": proof_valu,
         "end_to_end": {"value": round(n_constraints / (t_wit + ms / 1e3), 1), "unit": "constraints/s",
                        "note": "host witness synthesis (native; serial MiMC recurrence, rows/densities/constants on several threads) + upload + prover core"},
         "cpu_baseline": base,
