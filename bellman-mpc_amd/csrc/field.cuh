@@ -330,6 +330,65 @@ struct FpOps {
   static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<FpCfg>(a, w); }
 };
 
+// Fp2 product a*b = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u with Karatsuba's three column sums
+// shared by both halves: per column t0 = sum a0 b0, t1 = sum a1 b1, t2 = sum (a0+a1)(b0+b1);
+// c1 += t2 - t0 - t1 (exact: the true value is >= 0 and < 2^63), c0 += t0 - t1 on a signed
+// accumulator; both halves get their own interleaved Montgomery reduction.  c0 = (X + M p)/R
+// with X > -(128p)^2 lies in (-p/2^11, 2p): one conditional +p makes it >= 0.  Inputs < 128p
+// with 29-bit limbs (so a0+a1 limbs < 2^30, products < 2^60, 14-term columns < 2^63.9).
+template <class C>
+BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, const Fe<C>& b1, Fe<C>& r0,
+                         Fe<C>& r1) {
+  constexpr int N = C::N;
+  uint32_t sa[N], sb[N], m0[N], m1[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    sa[i] = a0.v[i] + a1.v[i];
+    sb[i] = b0.v[i] + b1.v[i];
+  }
+  int64_t acc0 = 0;
+  uint64_t acc1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t t0 = 0, t1 = 0, t2 = 0;
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+      t0 += (uint64_t)a0.v[i] * b0.v[k - i];
+      t1 += (uint64_t)a1.v[i] * b1.v[k - i];
+      t2 += (uint64_t)sa[i] * sb[k - i];
+    }
+    acc0 += (int64_t)(t0 - t1);
+    acc1 += t2 - t0 - t1;
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) {
+      acc0 += (int64_t)((uint64_t)m0[i] * C::P[k - i]);
+      acc1 += (uint64_t)m1[i] * C::P[k - i];
+    }
+    if (k < N) {
+      m0[k] = ((uint32_t)acc0 * C::INV) & BH_LIMB_MASK;
+      acc0 += (int64_t)((uint64_t)m0[k] * C::P[0]);
+      m1[k] = ((uint32_t)acc1 * C::INV) & BH_LIMB_MASK;
+      acc1 += (uint64_t)m1[k] * C::P[0];
+    } else {
+      r0.v[k - N] = (uint32_t)acc0 & BH_LIMB_MASK;
+      r1.v[k - N] = (uint32_t)acc1 & BH_LIMB_MASK;
+    }
+    acc0 >>= BH_LIMB_BITS;
+    acc1 >>= BH_LIMB_BITS;
+  }
+  r1.v[N - 1] = (uint32_t)acc1;
+  // r0's top limb is the signed remainder; add p when it is negative
+  const uint32_t neg = (uint32_t)(acc0 >> 63);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) {
+    const uint32_t s = r0.v[i] + (C::P[i] & neg) + c;
+    r0.v[i] = s & BH_LIMB_MASK;
+    c = s >> BH_LIMB_BITS;
+  }
+  r0.v[N - 1] = (uint32_t)acc0 + (C::P[N - 1] & neg) + c;
+}
+
 constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
   uint32_t r = 1;
   while (r < x) r <<= 1;
@@ -339,13 +398,12 @@ constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
 struct Fp2Ops {
   using T = DFp2;
   static constexpr uint32_t MB = 2;
-  // Schoolbook over two interleaved reductions: c0 = a0 b0 + (128p - a1) b1, c1 = a0 b1 + a1 b0.
-  // One reduction fewer than Karatsuba's three muls, no pre-additions, and both halves
-  // come out < 2p; valid for inputs < 128p.
+  // Column-wise Karatsuba (fe2_mul_kara): 3 x 196 product v_mad_u64_u32 + 2 reductions instead of
+  // the schoolbook 4 x 196 (two fe_mul2 of c0 = a0 b0 + (128p - a1) b1, c1 = a0 b1 + a1 b0);
+  // G2 accumulation alone 15.5 -> 14.9 ms per 2^22 proof.  Both halves < 2p; inputs < 128p.
   static BH_DEV T mul(const T& a, const T& b) {
     T r;
-    r.c0 = fe_mul2<FpCfg>(a.c0, b.c0, fe_neg<FpCfg, 128>(a.c1), b.c1);
-    r.c1 = fe_mul2<FpCfg>(a.c0, b.c1, a.c1, b.c0);
+    fe2_mul_kara<FpCfg>(a.c0, a.c1, b.c0, b.c1, r.c0, r.c1);
     return r;
   }
   static BH_DEV T sqr(const T& a) {
