@@ -398,12 +398,22 @@ constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
 struct Fp2Ops {
   using T = DFp2;
   static constexpr uint32_t MB = 2;
-  // Column-wise Karatsuba (fe2_mul_kara): 3 x 196 product v_mad_u64_u32 + 2 reductions instead of
-  // the schoolbook 4 x 196 (two fe_mul2 of c0 = a0 b0 + (128p - a1) b1, c1 = a0 b1 + a1 b0);
-  // G2 accumulation alone 15.5 -> 14.9 ms per 2^22 proof.  Both halves < 2p; inputs < 128p.
+  // Schoolbook over two interleaved reductions (c0 = a0 b0 + (128p - a1) b1, c1 = a0 b1 + a1 b0),
+  // or, in translation units that define BH_FP2_KARATSUBA (the G2 bucket accumulation,
+  // msm_g2_acc.hip), the column-wise Karatsuba fe2_mul_kara: 3 x 196 product v_mad_u64_u32
+  // instead of 4 x 196 (G2 accumulation alone 15.5 -> 14.9 ms per 2^22 proof).  The reduction
+  // kernels keep the schoolbook form: Karatsuba's extra live registers raised their spill
+  // scratch (k_reduce_blocks<G2> 2352 -> 2648 B/lane, k_cont_seq 32 -> 528) and a test run hit
+  // HSA_STATUS_ERROR_OUT_OF_RESOURCES launching k_reduce_window<G2>.  Both forms give < 2p for
+  // inputs < 128p (possibly different representatives of the same element).
   static BH_DEV T mul(const T& a, const T& b) {
     T r;
+#ifdef BH_FP2_KARATSUBA
     fe2_mul_kara<FpCfg>(a.c0, a.c1, b.c0, b.c1, r.c0, r.c1);
+#else
+    r.c0 = fe_mul2<FpCfg>(a.c0, b.c0, fe_neg<FpCfg, 128>(a.c1), b.c1);
+    r.c1 = fe_mul2<FpCfg>(a.c0, b.c1, a.c1, b.c0);
+#endif
     return r;
   }
   static BH_DEV T sqr(const T& a) {

@@ -1,5 +1,7 @@
 // G2Ops instantiation of the device MSM, part 1: workspace, digit sort and the bucket
-// accumulation kernels (see msm_impl.cuh).
+// accumulation kernels (see msm_impl.cuh).  The accumulation's Fp2 products use the column-wise
+// Karatsuba form (field.cuh); every kernel of this unit is emitted here only.
+#define BH_FP2_KARATSUBA 1
 #include "msm_impl.cuh"
 
 namespace bh {
