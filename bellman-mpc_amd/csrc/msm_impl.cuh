@@ -239,7 +239,12 @@ __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, c
   const uint32_t i = threadIdx.x;
   const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
   const uint32_t gb0 = w * NB + (blk * blockDim.x + i) * L;
+  // G2 (448-byte points, one wave per SIMD): the running total `acc` waits in this thread's LDS
+  // slot (free until the epilogue) instead of registers, which the compiler otherwise spills
+  // to scratch (KB per lane)
+  constexpr bool acc_lds = sizeof(typename C::P) > 256;
   typename C::P run = C::identity(), acc = C::identity(), bk = C::identity();
+  if (acc_lds) store_point<C>(&lds[i], acc);
   // per bucket k = L-1 .. 0:  bk = partial (+ each continuation partial);  run += bk;  acc += run
   int k = (int)L - 1;
   uint32_t op = 0, c_next = 0, c_end = 0;  // op 0: load, 1: continuation, 2: run, 3: acc
@@ -261,7 +266,7 @@ __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, c
     }
     if (op == 1) { a = bk; b = load_point<C>(&conts[c_next]); }
     else if (op == 2) { a = run; b = bk; }
-    else { a = acc; b = run; }
+    else { a = acc_lds ? load_point<C>(&lds[i]) : acc; b = run; }
     const typename C::P r = C::add(a, b);
     if (op == 1) {
       bk = r;
@@ -270,11 +275,14 @@ __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, c
       run = r;
       op = 3;
     } else {
-      acc = r;
+      if (acc_lds) store_point<C>(&lds[i], r);
+      else acc = r;
       op = 0;
       k--;
     }
   }
+  if (acc_lds) acc = load_point<C>(&lds[i]);
+  __syncthreads();  // every thread has its acc back before the epilogue reuses the slots
   typename C::P s_blk;
   block_epilogue<C>(run, acc, lgL, acc, -1, false, lds, &s_blk);
   if (i == 0) {
