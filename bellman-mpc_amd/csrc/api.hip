@@ -708,7 +708,8 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess ||
-      hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->host_spans, 8 * MAX_SPAN_BLOCKS * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
     release_mask(c); delete c;
     return BH_ERR_OUT_OF_MEMORY;
   }
@@ -740,6 +741,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (ctx->host_out1) (void)hipHostFree(ctx->host_out1);
   if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
   if (ctx->host_counts) (void)hipHostFree(ctx->host_counts);
+  if (ctx->host_spans) (void)hipHostFree(ctx->host_spans);
   (void)hipStreamDestroy(ctx->stream);
   if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
   (void)hipStreamDestroy(ctx->stream2);

@@ -157,9 +157,9 @@ struct bh_ctx {
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
   double last_timings[16] = {};  // bh_last_timings [0,10) + bh_last_stats extras
-  uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp,
-                                    // [16,32) its continuation span (max_span)
-  bh::DevBuf dspan;                 // device words for max_span
+  uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp
+  uint32_t* host_spans = nullptr;   // pinned: MAX_SPAN_BLOCKS per-workgroup max_span words per prover multiexp
+  bh::DevBuf dspan;                 // device words for max_span (the same layout)
   std::vector<bh_ctx*> vranks;      // bh_prove_witness_partials_local: the virtual ranks' contexts
   std::vector<bh_ctx*> lanes;       // bh_prove_batch: the lanes' contexts
   // host -> device staging of caller buffers (bh_prove, bh_witness_upload): H2D copy stream,

@@ -92,10 +92,23 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
                     int max_span = -1);
 
 size_t scan_scratch_words(size_t n);
-// max over buckets of (last segment - first segment) for segment length S, into d_word and
-// (pinned) *h_word, stream-ordered: the continuation-tree depth msm_back needs
-hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_word,
-                    uint32_t* h_word, hipStream_t st);
+// max over buckets of (last segment - first segment) for segment length S: the
+// continuation-tree depth msm_back needs.  Each of max_span_blocks(nbt) workgroups writes its
+// own maximum to d_words[b] and the (pinned) h_words receive them, stream-ordered; the host takes
+// the max (max_span_host).  No zero-initialised word, so no fill kernel ahead of it: on a side
+// stream beside a whole-GPU accumulation every extra dispatch waits for a free slot.
+constexpr uint32_t MAX_SPAN_BLOCKS = 256;
+inline uint32_t max_span_blocks(size_t nbt) {
+  const size_t g = (nbt + 255) / 256;
+  return (uint32_t)(g < 1 ? 1 : (g > MAX_SPAN_BLOCKS ? MAX_SPAN_BLOCKS : g));
+}
+inline uint32_t max_span_host(const uint32_t* h_words, size_t nbt) {
+  uint32_t m = 0;
+  for (uint32_t b = 0, g = max_span_blocks(nbt); b < g; b++) m = h_words[b] > m ? h_words[b] : m;
+  return m;
+}
+hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_words,
+                    uint32_t* h_words, hipStream_t st);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st);
 hipError_t scalars_prepare(const uint32_t* d_in, uint32_t* d_out, size_t n, int mode, int log_perm, hipStream_t st);
 hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset, int32_t* d_idx, uint32_t* d_tmp,

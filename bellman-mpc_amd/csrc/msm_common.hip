@@ -321,6 +321,8 @@ __global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, siz
   }
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < P; p += 256) tilecounts[(size_t)p * ntiles + blockIdx.x] = hist[p];
+  // the scan's extra last word (its output is the total): zeroed here rather than by a fill
+  if (blockIdx.x == 0 && threadIdx.x == 0) tilecounts[(size_t)P * ntiles] = 0;
 }
 
 __global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, size_t n, const int32_t* idx,
@@ -486,7 +488,6 @@ hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_id
   uint32_t P, nt;
   sort_geometry(sh, n, &lo, &P, &nt);
   const size_t tw = (size_t)P * nt + 1;
-  hipMemsetAsync(tilecounts + tw - 1, 0, 4, st);
   if (n == 0) {
     hipMemsetAsync(counts, 0, (nbt + 1) * 4, st);
     hipMemsetAsync(offsets, 0, (nbt + 1) * 4, st);
@@ -520,17 +521,19 @@ __global__ void __launch_bounds__(256) k_max_span(const uint32_t* counts, const 
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+  __shared__ uint32_t wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));  // every block writes
 }
 
-hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_word,
-                    uint32_t* h_word, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(d_word, 0, 4, st);
-  if (e != hipSuccess) return e;
-  const unsigned g = (unsigned)std::min<size_t>(1024, (nbt + 255) / 256);
-  hipLaunchKernelGGL(k_max_span, dim3(std::max(1u, g)), dim3(256), 0, st, counts, offsets, nbt, S, d_word);
-  if (h_word) e = hipMemcpyAsync(h_word, d_word, 4, hipMemcpyDeviceToHost, st);
-  return e != hipSuccess ? e : hipGetLastError();
+hipError_t max_span(const uint32_t* counts, const uint32_t* offsets, size_t nbt, uint32_t S, uint32_t* d_words,
+                    uint32_t* h_words, hipStream_t st) {
+  const unsigned g = max_span_blocks(nbt);
+  hipLaunchKernelGGL(k_max_span, dim3(g), dim3(256), 0, st, counts, offsets, nbt, S, d_words);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && h_words) e = hipMemcpyAsync(h_words, d_words, g * 4, hipMemcpyDeviceToHost, st);
+  return e;
 }
 
 hipError_t density_index(const uint64_t* d_words, size_t n, uint32_t base_offset, int32_t* d_idx, uint32_t* d_tmp,

@@ -581,7 +581,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(ctx->idx.alloc(maxn * 4));
   BH_TRY_HIP(ctx->dtmp.alloc((maxn / 64 + 2) * 4));
   BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(maxn / 64 + 2) * 4 + 64));
-  BH_TRY_HIP(ctx->dspan.alloc(16 * 4));
+  BH_TRY_HIP(ctx->dspan.alloc(8 * MAX_SPAN_BLOCKS * 4));
 
   // ---- error semantics (prover.rs:309-343 order: delta check, then the waits)
   const uint64_t* dens = w->dens.as<uint64_t>();
@@ -822,8 +822,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const MsmShape& shj = shapes[j];
     const uint32_t* cnt = J.g2 ? ctx->pw2[J.out].counts : ctx->pw1[J.out].counts;
     const uint32_t* off = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
-    BH_TRY_HIP(max_span(cnt, off, (size_t)shj.Wb * shj.NB, (uint32_t)shj.S, ctx->dspan.as<uint32_t>() + j,
-                        ctx->host_counts + 16 + j, st));
+    BH_TRY_HIP(max_span(cnt, off, (size_t)shj.Wb * shj.NB, (uint32_t)shj.S,
+                        ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS, ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS,
+                        st));
     BH_TRY_HIP(hipEventRecord(jev[16 + j], st));
     return BH_OK;
   };
@@ -860,7 +861,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     int span = -1;
     if (n >= SMALL_JOB) {  // the sort ran ahead; its span word is on the host once it is done
       BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
-      span = (int)ctx->host_counts[16 + j];
+      span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS, (size_t)shapes[j].Wb * shapes[j].NB);
     }
     if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span));
     else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span));
@@ -959,10 +960,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   const auto t_acc0 = std::chrono::steady_clock::now();
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
   if (h_mode == 3 && (s = enqueue_h(jev[33]))) return s;
+  const auto t_h = std::chrono::steady_clock::now();
   for (int r = pre_sorts; r < ns; r++) {
     if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
     if ((s = sort_job(sorder[r], sS))) return s;
   }
+  const auto t_sorts = std::chrono::steady_clock::now();
   for (int q = 1; q < nbig; q++)
     if ((s = acc_job(big[q], sA))) return s;
   if (nbig > 0) last_acc = big[nbig - 1];
@@ -1009,8 +1012,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, enqueue done %.3f, gpu and combines done %.3f, after %.3f\n",
-            ms(t0, t_acc0), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
+    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, H %.3f, sorts %.3f, enqueue done %.3f, gpu and combines done %.3f, after %.3f\n",
+            ms(t0, t_acc0), ms(t0, t_h), ms(t0, t_sorts), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
   }
   float h_ms = 0;
   hipEventElapsedTime(&h_ms, ctx->ev[0], ctx->ev[1]);
