@@ -317,15 +317,21 @@ class Waiter:
     """multicore.rs:94-110: the pending result of multiexp_async; wait() returns the
     uncompressed affine point (or raises the multiexp's SynthesisError)."""
 
-    def __init__(self, handle, group):
-        self.h, self.group = handle, group
+    def __init__(self, handle, group, ctx=None, bases=None):
+        # the context and bases stay referenced until the wait: garbage collection cannot
+        # destroy them under a multiexp in flight (an explicit ctx.close() detaches the job:
+        # wait() then raises)
+        self.h, self.group, self._ctx, self._bases = handle, group, ctx, bases
 
     def wait(self):
         if self.h is None:
             raise RuntimeError("Waiter already waited")
         out = np.zeros(96 if self.group == BH_G1 else 192, dtype=np.uint8)
         h, self.h = self.h, None
-        _check(_lib.bh_multiexp_wait(h, _ptr(out)), "bh_multiexp_wait")
+        try:
+            _check(_lib.bh_multiexp_wait(h, _ptr(out)), "bh_multiexp_wait")
+        finally:
+            self._ctx = self._bases = None
         return out.tobytes()
 
     def __del__(self):
@@ -352,7 +358,7 @@ def multiexp_async(ctx, bases, offset, density, exponents, montgomery=False):
                                    _ptr(ex) if n else None, n,
                                    BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, ctypes.byref(h)),
            "bh_multiexp_submit")
-    return Waiter(h, bases.group)
+    return Waiter(h, bases.group, ctx, bases)
 
 
 # ------------------------------------------------------------------ EvaluationDomain

@@ -625,11 +625,19 @@ int bh_version(void) { return 1; }
 // tails (measured in a kernel trace: queue ids shared by streams 6/7, 4/9, 5/8).  Raise the
 // value to 16 when it is lower (BH_KEEP_HW_QUEUES=1 keeps the environment's value); this runs
 // when the library is loaded, before the runtime reads it at its first HIP call.
+// A value the caller set explicitly below 16 is still raised (the GPU box exports 4), but never
+// silently: the override is reported once on stderr (include/bellman_hip.h documents the rule;
+// the bench line records the environment's value and the effective one).
 __attribute__((constructor)) static void bh_hw_queues() {
+  const char* cur = getenv("GPU_MAX_HW_QUEUES");
   const char* keep = getenv("BH_KEEP_HW_QUEUES");
   if (keep && keep[0] == '1') return;
-  const char* cur = getenv("GPU_MAX_HW_QUEUES");
-  if (!cur || atoi(cur) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+  if (!cur || atoi(cur) < 16) {
+    setenv("GPU_MAX_HW_QUEUES", "16", 1);
+    if (cur)
+      fprintf(stderr, "bellman_hip: GPU_MAX_HW_QUEUES=%s raised to 16 for this process (the prover's concurrent "
+                      "streams need their own hardware queues; BH_KEEP_HW_QUEUES=1 keeps %s)\n", cur, cur);
+  }
 }
 
 static std::atomic<int> g_masked_ctxs[64];  // live CU-masked contexts per device (0 or 1)

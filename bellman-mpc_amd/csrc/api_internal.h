@@ -69,6 +69,16 @@ struct DistH;
 }  // namespace bh
 
 struct bh_job_slot;  // jobs.hip: one in-flight async multiexp's stream, workspace and buffers
+struct bh_job;
+// jobs.hip: the async multiexps' recycled slots and the jobs not yet waited for.  Shared by the
+// context and every outstanding job, so it outlives bh_ctx_destroy: a job of a destroyed
+// context is detached (its wait reports an error and touches nothing of the context).
+struct bh_job_registry {
+  std::mutex mu;
+  bool alive = true;                       // false once the context is destroyed
+  std::vector<bh_job_slot*> all_slots, free_slots;
+  std::vector<bh_job*> pending;            // submitted, not yet waited for
+};
 
 struct bh_srs {
   bh_ctx* ctx = nullptr;
@@ -168,10 +178,9 @@ struct bh_ctx {
   bh::H2DRing ring;
   std::unique_ptr<bh::HostPool> pool;
   bh_witness* dropin = nullptr;
-  // bh_multiexp_submit / _wait (jobs.hip): recycled per-job resources, their own lock (a
+  // bh_multiexp_submit / _wait (jobs.hip): recycled per-job resources under their own lock (a
   // submit never waits behind a proof holding mu)
-  std::mutex jobs_mu;
-  std::vector<bh_job_slot*> all_slots, free_slots;
+  std::shared_ptr<bh_job_registry> jobs = std::make_shared<bh_job_registry>();
   std::mutex mu;
 };
 

@@ -8,6 +8,8 @@
 // beside accumulations of another), as the reference's rayon tasks do on the CPU.
 #include <string.h>
 
+#include <algorithm>
+
 #include "api_internal.h"
 
 using namespace bh;
@@ -29,22 +31,25 @@ struct bh_job_slot {
 };
 
 struct bh_job {
-  bh_ctx* ctx = nullptr;
+  std::shared_ptr<bh_job_registry> reg;  // keeps the slot bookkeeping alive past bh_ctx_destroy
+  int device = 0;
+  int window_override = 0;
   bh_job_slot* slot = nullptr;
   int group = BH_G1;
   MsmShape sh{};
-  bool empty = false;     // n == 0: the identity
+  bool empty = false;      // n == 0: the identity
+  bool detached = false;   // the context was destroyed before wait (the slot was released with it)
   bh_status status = BH_OK;  // deferred error (the reference reports it from wait())
 };
 
 namespace {
 
-bh_status take_slot(bh_ctx* ctx, bh_job_slot** out) {
+bh_status take_slot(bh_job_registry& reg, bh_job_slot** out) {
   {
-    std::lock_guard<std::mutex> lk(ctx->jobs_mu);
-    if (!ctx->free_slots.empty()) {
-      *out = ctx->free_slots.back();
-      ctx->free_slots.pop_back();
+    std::lock_guard<std::mutex> lk(reg.mu);
+    if (!reg.free_slots.empty()) {
+      *out = reg.free_slots.back();
+      reg.free_slots.pop_back();
       return BH_OK;
     }
   }
@@ -52,21 +57,28 @@ bh_status take_slot(bh_ctx* ctx, bh_job_slot** out) {
   BH_TRY_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
   BH_TRY_HIP(hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
   *out = s.release();
-  std::lock_guard<std::mutex> lk(ctx->jobs_mu);
-  ctx->all_slots.push_back(*out);
+  std::lock_guard<std::mutex> lk(reg.mu);
+  reg.all_slots.push_back(*out);
   return BH_OK;
 }
 
-void give_slot(bh_ctx* ctx, bh_job_slot* s) {
-  std::lock_guard<std::mutex> lk(ctx->jobs_mu);
-  ctx->free_slots.push_back(s);
+// back to the free list, or -- the context is gone -- released
+void give_slot(bh_job_registry& reg, bh_job_slot* s) {
+  {
+    std::lock_guard<std::mutex> lk(reg.mu);
+    if (reg.alive) {
+      reg.free_slots.push_back(s);
+      return;
+    }
+    reg.all_slots.erase(std::remove(reg.all_slots.begin(), reg.all_slots.end(), s), reg.all_slots.end());
+  }
+  delete s;
 }
 
 template <class C>
 bh_status enqueue_msm(bh_job* job, MsmWorkspace<C>& ws, const bh_srs* bases, size_t base_offset, size_t n,
                       const int32_t* d_idx) {
-  bh_ctx* ctx = job->ctx;
-  job->sh = msm_shape(n, ctx->window_override);
+  job->sh = msm_shape(n, job->window_override);
   fit_segments<C>(job->sh, n);
   BH_TRY_HIP(msm_window_sums<C>(ws, job->slot->st, bases->pts.as<uint32_t>(), job->slot->scalars.as<uint32_t>(), n,
                                 d_idx, (uint32_t)base_offset, job->sh, nullptr));
@@ -75,11 +87,26 @@ bh_status enqueue_msm(bh_job* job, MsmWorkspace<C>& ws, const bh_srs* bases, siz
 
 }  // namespace
 
+// bh_ctx_destroy: every job not yet waited for is detached and its slot released (after its
+// stream drains); slots a waiter currently holds are released by that waiter (give_slot)
 void bh_ctx_release_jobs(bh_ctx* ctx) {
-  std::lock_guard<std::mutex> lk(ctx->jobs_mu);
-  for (bh_job_slot* s : ctx->all_slots) delete s;
-  ctx->all_slots.clear();
-  ctx->free_slots.clear();
+  std::vector<bh_job_slot*> dead;
+  {
+    std::lock_guard<std::mutex> lk(ctx->jobs->mu);
+    bh_job_registry& reg = *ctx->jobs;
+    reg.alive = false;
+    for (bh_job* j : reg.pending) {
+      j->detached = true;
+      if (j->slot) dead.push_back(j->slot);
+      j->slot = nullptr;
+    }
+    reg.pending.clear();
+    for (bh_job_slot* s : reg.free_slots) dead.push_back(s);
+    reg.free_slots.clear();
+    for (bh_job_slot* s : dead)
+      reg.all_slots.erase(std::remove(reg.all_slots.begin(), reg.all_slots.end(), s), reg.all_slots.end());
+  }
+  for (bh_job_slot* s : dead) delete s;  // ~bh_job_slot drains the slot's stream first
 }
 
 extern "C" {
@@ -93,7 +120,9 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
   if (n > 0x7fffffffull || !bases->ctx || bases->ctx->device != ctx->device) return BH_ERR_INVALID_ARGUMENT;
   BH_TRY_HIP(hipSetDevice(ctx->device));
   std::unique_ptr<bh_job> job(new bh_job());
-  job->ctx = ctx;
+  job->reg = ctx->jobs;
+  job->device = ctx->device;
+  job->window_override = ctx->window_override;
   job->group = bases->group;
   // Source semantics (EOF / identity base): decided on the host from the density map and, only
   // when an identity base is reachable, the exponents; reported by wait() like the reference
@@ -114,12 +143,12 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
     *out = job.release();
     return BH_OK;
   }
-  bh_status s = take_slot(ctx, &job->slot);
+  bh_status s = take_slot(*job->reg, &job->slot);
   if (s) return s;
   bh_job_slot* sl = job->slot;
   auto fail = [&](bh_status e) {
     (void)hipStreamSynchronize(sl->st);
-    give_slot(ctx, sl);
+    give_slot(*job->reg, sl);
     return e;
   };
   // the caller's buffers are read before submit returns (pageable copies complete on return)
@@ -144,6 +173,10 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
                             : enqueue_msm<G2Ops>(job.get(), sl->ws2, bases, base_offset, n, d_idx);
   if (s) return fail(s);
   if (hipEventRecord(sl->done, sl->st)) return fail(BH_ERR_HIP);
+  {
+    std::lock_guard<std::mutex> lk(job->reg->mu);
+    job->reg->pending.push_back(job.get());
+  }
   *out = job.release();
   return BH_OK;
 }
@@ -151,7 +184,6 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
 bh_status bh_multiexp_wait(bh_job* job, uint8_t* out) {
   if (!job) return BH_ERR_INVALID_ARGUMENT;
   std::unique_ptr<bh_job> j(job);
-  bh_ctx* ctx = j->ctx;
   if (j->empty) {
     if (j->status) return j->status;
     if (!out) return BH_ERR_INVALID_ARGUMENT;
@@ -159,14 +191,22 @@ bh_status bh_multiexp_wait(bh_job* job, uint8_t* out) {
     else g2_to_uncompressed(jac_to_affine(jac_identity<bh::Fp2>()), out);
     return BH_OK;
   }
-  bh_job_slot* sl = j->slot;
+  bh_job_slot* sl = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(j->reg->mu);
+    auto& pend = j->reg->pending;
+    pend.erase(std::remove(pend.begin(), pend.end(), j.get()), pend.end());
+    if (!j->detached) sl = j->slot;
+  }
+  if (!sl) return BH_ERR_INVALID_ARGUMENT;  // its context was destroyed: no result exists
+  (void)hipSetDevice(j->device);
   const hipError_t e = hipEventSynchronize(sl->done);  // Waiter::wait: a host-side event sync
   bh_status s = e == hipSuccess ? BH_OK : BH_ERR_HIP;
   if (!s && out) {
     if (j->group == BH_G1) g1_to_uncompressed(jac_to_affine(combine_g1(sl->ws1.host_window_sums, j->sh)), out);
     else g2_to_uncompressed(jac_to_affine(combine_g2(sl->ws2.host_window_sums, j->sh)), out);
   }
-  give_slot(ctx, sl);
+  give_slot(*j->reg, sl);
   if (!out && !s) return BH_ERR_INVALID_ARGUMENT;
   return s;
 }

@@ -562,6 +562,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                        Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
                        UploadSync* up = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
+  bh_params* mparams = const_cast<bh_params*>(params);
+  // The proof reads the Parameters' window tables under a shared lock (taken below).  Declared
+  // before the drain guard so that on an error return the streams are drained BEFORE the lock
+  // is released: another context must not rebuild a table that kernels of this failed proof
+  // may still be reading.
+  std::shared_lock<std::shared_mutex> prd(mparams->mu, std::defer_lock);
   // an error return in the middle of enqueueing leaves kernels running on the streams below,
   // reading workspaces the next call reuses: drain every stream before returning one
   struct DrainOnError {
@@ -569,7 +575,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     bool ok = false;
     ~DrainOnError() { if (!ok) ctx_sync_all(c); }
   } drain{ctx};
-  bh_params* mparams = const_cast<bh_params*>(params);
   const size_t m = w->m, ni = w->num_inputs, na = w->num_aux;
   const int L = w->log_m;
   bh_status s;
@@ -654,7 +659,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // tables it wants but lacks are built first under the exclusive lock (a proof of another
   // shape may have replaced them).
   Job jobs[8];
-  std::shared_lock<std::shared_mutex> prd(mparams->mu);
+  prd.lock();
   if ((s = plan_shard(ctx, params, w, shard, nshards, sg, sh_buf, sh_idx, idx_aaux, idx_bin, idx_baux, false, jobs)))
     return s;
   if (may_build && plan_needs_build(params, jobs, sg, ctx->tables && !ctx->window_override)) {

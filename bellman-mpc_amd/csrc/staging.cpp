@@ -7,73 +7,6 @@
 
 namespace bh {
 
-HostPool::HostPool(int workers) {
-  for (int i = 0; i < workers; i++) threads_.emplace_back([this] { run(); });
-}
-
-HostPool::~HostPool() {
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    stop_ = true;
-  }
-  cv_.notify_all();
-  for (auto& t : threads_) t.join();
-}
-
-void HostPool::run() {
-  size_t seen = 0;
-  for (;;) {
-    const std::function<void(int)>* fn;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-      if (stop_) return;
-      seen = gen_;
-      fn = fn_;
-      active_++;
-    }
-    for (;;) {
-      int i;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (next_ >= n_) break;
-        i = next_++;
-      }
-      (*fn)(i);
-    }
-    std::lock_guard<std::mutex> lk(mu_);
-    if (--active_ == 0) done_cv_.notify_all();
-  }
-}
-
-void HostPool::parallel_for(int n, const std::function<void(int)>& fn) {
-  if (n <= 0) return;
-  if (threads_.empty() || n == 1) {
-    for (int i = 0; i < n; i++) fn(i);
-    return;
-  }
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    fn_ = &fn;
-    n_ = n;
-    next_ = 0;
-    gen_++;
-  }
-  cv_.notify_all();
-  for (;;) {  // the caller works too
-    int i;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (next_ >= n_) break;
-      i = next_++;
-    }
-    fn(i);
-  }
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return active_ == 0 && next_ >= n_; });
-  fn_ = nullptr;
-}
-
 hipError_t H2DRing::init() {
   if (buf[0]) return hipSuccess;
   for (int k = 0; k < SLOTS; k++) {

@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on a bounded sample (rank 0)")
     ap.add_argument("--cpu-log-constraints", type=int, default=16)
     ap.add_argument("--cpu-1t-log-constraints", type=int, default=12, help="1-thread CPU sample (0: skip)")
+    ap.add_argument("--cpu-full", type=int, default=0,
+                    help="also time the CPU port once on the bench's own workload (2^22: ~1 min on 256 threads, "
+                         "~8 min on the GPU box's 16-thread share; the committed run is "
+                         "profiles/r03_cpu_baseline_2p22.json)")
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
     ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
     ap.add_argument("--c5", type=int, default=64,
@@ -93,16 +97,24 @@ def cpu_topology():
     return len(cores) or None, len(sockets) or None
 
 
-def cpu_baseline(bh, ctx, log_c, log_c_1t):
+def cpu_threads(cpu_port):
+    """The host threads the CPU baseline may use: the box's CPU share when the environment
+    states it (OMP_NUM_THREADS: 16 per GPU on the GPU pool), else every hardware thread."""
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return int(share) if share.isdigit() and int(share) > 0 else cpu_port.hardware_threads()
+
+
+def cpu_baseline(bh, ctx, log_c, log_c_1t, full=None):
     """bench leg only: the oracle's C++ port of bellman's multicore prover core
     (oracle/cpu/bellman_port.cpp), timed on this host's cores on a bounded sample
     (a 2^log_c-constraint MiMC chain, median of 3 after the port's own warm-up), plus a
-    1-thread figure on a smaller sample.  Its proofs must equal the GPU's."""
+    1-thread figure on a smaller sample, and (full = (params, rounds, proof)) one run at the
+    headline size.  Its proofs must equal the GPU's."""
     from oracle import cpu_port
     rounds = (1 << (log_c - 1)) - 1
     params = bh.Parameters.chain(ctx, rounds)
     gpu_proof = bh.prove_witness(ctx, params, bh.Witness.chain(ctx, rounds), 27134, 17146)
-    threads = cpu_port.hardware_threads()
+    threads = cpu_threads(cpu_port)
     reps = 3
     t0 = time.time()
     proof, ms, ms_syn = cpu_port.chain_prove(params.write(), rounds, threads=threads, reps=reps)
@@ -110,7 +122,8 @@ def cpu_baseline(bh, ctx, log_c, log_c_1t):
     n_c = 2 * rounds + 2
     phys, sockets = cpu_topology()
     out = {"value": round(n_c / (ms / 1e3), 1), "unit": "constraints/s", "cores": threads, "kind": "port",
-           "threads_are": "hardware threads used (SMT siblings included)", "physical_cores": phys,
+           "threads_are": "host threads used: the box's CPU share (OMP_NUM_THREADS) when set, else every "
+                          "hardware thread", "machine_physical_cores": phys,
            "sockets": sockets, "cpu_model": cpu_model(),
            "sample": f"median of {reps} prover-core runs (assignment -> proof) of a 2^{log_c}-constraint "
                      f"MiMC chain; bellman's multicore algorithm restated in C++ (oracle/cpu); "
@@ -118,13 +131,32 @@ def cpu_baseline(bh, ctx, log_c, log_c_1t):
            "ms_per_proof": round(ms, 1), "synthesis_ms": round(ms_syn, 1),
            "end_to_end_value": round(n_c / ((ms + ms_syn) / 1e3), 1),
            "proof_matches_gpu": proof == gpu_proof}
-    full = os.path.join(ROOT, "profiles", "r02_cpu_baseline_2p22.json")
-    if os.path.exists(full):  # the same port once at the headline size (tools/cpu_baseline_full.py)
-        with open(full) as f:
-            fr = json.loads(f.read().strip().splitlines()[-1])
-        out["headline_size_run"] = {k: fr.get(k) for k in ("log_constraints", "value", "ms_per_proof", "threads",
-                                                            "physical_cores", "sockets", "proof_matches_gpu")}
-        out["headline_size_run"]["source"] = "profiles/r02_cpu_baseline_2p22.json (a committed earlier run)"
+    if full is not None:
+        # the same port once at the headline size, in this run: the bench's own 2^22 Parameters
+        # and chain, the same threads; its proof must equal the bench's proof
+        fparams, frounds, fproof = full
+        t0 = time.time()
+        pbytes = fparams.write()
+        proof_f, ms_f, syn_f = cpu_port.chain_prove(pbytes, frounds, threads=threads, reps=1)
+        del pbytes
+        nf = 2 * frounds + 2
+        out["headline_size_run"] = {"log_constraints": nf.bit_length() - 1, "value": round(nf / (ms_f / 1e3), 1),
+                                    "unit": "constraints/s", "ms_per_proof": round(ms_f, 1),
+                                    "synthesis_ms": round(syn_f, 1), "threads": threads,
+                                    "sockets": sockets, "proof_matches_gpu": proof_f == fproof,
+                                    "wall_s": round(time.time() - t0, 1),
+                                    "source": "timed in this run (one prover-core run, after synthesis)"}
+    else:
+        for name in ("r03_cpu_baseline_2p22.json", "r02_cpu_baseline_2p22.json"):
+            path = os.path.join(ROOT, "profiles", name)
+            if os.path.exists(path):  # the same port once at the headline size (tools/cpu_baseline_full.py)
+                with open(path) as f:
+                    fr = json.loads(f.read().strip().splitlines()[-1])
+                out["headline_size_run"] = {k: fr.get(k) for k in ("log_constraints", "value", "ms_per_proof",
+                                                                    "threads", "physical_cores", "sockets",
+                                                                    "proof_matches_gpu")}
+                out["headline_size_run"]["source"] = f"profiles/{name} (a committed run; --cpu-full 1 times it here)"
+                break
     if log_c_1t:
         r1 = (1 << (log_c_1t - 1)) - 1
         p1 = bh.Parameters.chain(ctx, r1)
@@ -179,6 +211,11 @@ def main():
     except bh_launch.LaunchError as e:
         print(f"bench.py: {e}", file=sys.stderr)
         sys.exit(2)
+    # the hardware-queue setting the library will raise (include/bellman_hip.h), recorded as found
+    hwq_env = os.environ.get("GPU_MAX_HW_QUEUES")
+    hwq_keep = os.environ.get("BH_KEEP_HW_QUEUES") == "1"
+    hw_queues = {"env": hwq_env, "effective": hwq_env if hwq_keep or (hwq_env and int(hwq_env) >= 16) else "16",
+                 "raised_by_library": not hwq_keep and not (hwq_env and int(hwq_env) >= 16)}
     if spawn:
         # plain `python bench.py --gpus N`: start the N rank processes (one per GPU, LOCAL_RANK =
         # device) before this parent touches HIP, and exit with the first failing rank's code
@@ -203,8 +240,18 @@ def main():
     witness = bh.Witness.chain(ctx, rounds)
     t_wit = time.time() - t0
     t0 = time.time()
+    prepared = None
     if args.tables:
-        params.prepare(witness, world)  # SRS window tables: a function of the CRS only
+        # SRS window tables: a function of the CRS only.  A rank of an N-GPU run builds exactly
+        # the slices its shard reads (and, with the H block distributed, the table over its own
+        # share of h) -- the per-rank tables tools/shard_rehearsal.py times, 1/N of the memory
+        # and setup of the full tables
+        if world > 1:
+            params.prepare_shard(witness, rank, world, distributed_h=True)
+            prepared = "shard"
+        else:
+            params.prepare(witness)
+            prepared = "full"
     else:
         ctx.set_tables(False)
     t_tables = time.time() - t0
@@ -266,13 +313,16 @@ def main():
     elapsed = time.perf_counter() - t_start
     # window tables the timed proofs read (rank 0 of N, or every rank's own slices for N > 1)
     st = ctx.last_stats()
-    tables = {"used": int(st[10]), "large_multiexps": int(st[11]), "GB": round(st[12] / 1e9, 2)}
+    tables = {"used": int(st[10]), "large_multiexps": int(st[11]), "GB": round(st[12] / 1e9, 2),
+              "prepare": prepared, "setup_s": round(t_tables, 2)}
     per_rank_ms = None
     if comm is not None:
-        mine = [elapsed * 1000.0 / args.steps, tables["used"], tables["large_multiexps"], tables["GB"]]
-        recs = [json.loads(x.decode().strip()) for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(96))]
+        mine = [elapsed * 1000.0 / args.steps, tables["used"], tables["large_multiexps"], tables["GB"], prepared,
+                round(t_tables, 2)]
+        recs = [json.loads(x.decode().strip()) for x in comm.allgather_bytes(json.dumps(mine).encode().ljust(128))]
         per_rank_ms = [round(x[0], 3) for x in recs]
-        tables = {"used": [x[1] for x in recs], "large_multiexps": [x[2] for x in recs], "GB": [x[3] for x in recs]}
+        tables = {"used": [x[1] for x in recs], "large_multiexps": [x[2] for x in recs], "GB": [x[3] for x in recs],
+                  "prepare": [x[4] for x in recs], "setup_s": [x[5] for x in recs]}
         elapsed = comm.allreduce_max(elapsed)
     ms = elapsed * 1000.0 / args.steps
     value = n_constraints * args.steps / elapsed
@@ -353,7 +403,8 @@ def main():
         dropin["verify_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
         del asg
     # CPU baseline: rank 0 of a 1-GPU run only (a bounded sample; see cpu_baseline)
-    base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints)
+    base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints,
+                         (params, rounds, ref) if args.cpu_full else None)
             if args.cpu_baseline and world == 1 else None)
     out = {
         "metric": "Groth16 constraints/sec, BLS12-381, 2^22-constraint R1CS",
@@ -372,6 +423,7 @@ def main():
                    "constraints": n_constraints, "log_domain": k, "parallelism": f"msm-shard{world}",
                    "exchange": "rccl" if world > 1 else None},
         "rccl": rccl,
+        "gpu_max_hw_queues": hw_queues,
         "per_rank_ms_per_step": per_rank_ms,
         "srs_window_tables": tables,
         "dropin": dropin,

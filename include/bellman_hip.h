@@ -31,6 +31,14 @@
  *   - Group elements use the zcash/bls12_381 encodings (big-endian, flag bits
  *     in byte 0): uncompressed 96 B (G1) / 192 B (G2), compressed 48/96 B.
  *   - Every function returns a bh_status; it never aborts across the FFI.
+ *   - Process-wide side effect at load: GPU_MAX_HW_QUEUES is raised to 16 when it is
+ *     unset or lower (HIP's default is 4; the prover keeps up to 12 streams busy and
+ *     streams sharing a hardware queue serialise).  An explicitly set lower value is
+ *     overridden too, with one line on stderr; BH_KEEP_HW_QUEUES=1 keeps the environment's
+ *     value.  This only takes effect when the library loads before the first HIP call of
+ *     the process.  Queue budget per context: DESIGN.md section 5.
+ *   - bh_multiexp_submit jobs outlive nothing: destroying their context detaches every
+ *     job not yet waited for, whose bh_multiexp_wait then returns BH_ERR_INVALID_ARGUMENT.
  */
 #ifndef BELLMAN_HIP_H
 #define BELLMAN_HIP_H

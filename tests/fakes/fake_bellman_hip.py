@@ -44,25 +44,39 @@ class Context:
     def last_stats(self):
         return list(self._stats)
 
-    def _proved(self, n):
+    def _proved(self, n, table_bytes=0.0):
         time.sleep(0.001)
         self._stats = [1.0, 0.5, 0.8, 6, 6.0 * n, 0.2, 2, 1.0 * n, 13.0 * n, 2.0 * n,
-                       5 if self.tables else 0, 5, 1e9 if self.tables else 0.0]
+                       5 if self.tables else 0, 5, table_bytes if self.tables else 0.0]
 
     def close(self):
         pass
 
 
+FULL_TABLE_BYTES = 31.4e9  # the 2^22 proof's window tables on one device
+
+
 class Parameters:
+    """Records which window tables were prepared (`prepared`): ("full", nshards) for
+    bh_params_prepare, ("shard", shard, nshards, distributed_h) for bh_params_prepare_shard."""
+
     def __init__(self, ctx, rounds):
-        self.ctx, self.rounds = ctx, rounds
+        self.ctx, self.rounds, self.prepared = ctx, rounds, None
 
     @classmethod
     def chain(cls, ctx, rounds):
         return cls(ctx, rounds)
 
     def prepare(self, witness, nshards=1):
-        pass
+        self.prepared = ("full", nshards)
+
+    def prepare_shard(self, witness, shard, nshards, distributed_h=True):
+        self.prepared = ("shard", shard, nshards, bool(distributed_h))
+
+    def table_bytes(self):
+        if not self.prepared:
+            return 0.0
+        return FULL_TABLE_BYTES / self.prepared[2] if self.prepared[0] == "shard" else FULL_TABLE_BYTES
 
     def vk_bytes(self):
         return _h("vk", self.rounds, n=96 * 3 + 192 * 3 + 4 + 96 * 2)
@@ -78,7 +92,7 @@ class Witness:
 
 
 def prove_witness(ctx, params, w, r, s):
-    ctx._proved(2 * params.rounds + 2)
+    ctx._proved(2 * params.rounds + 2, params.table_bytes())
     return _h("proof", params.rounds, w.seed, w.preimage_seed, r, s)
 
 
@@ -124,7 +138,12 @@ class Comm:
         return (self.nranks, self.rank, self.ctx.device)
 
     def prove_partial(self, ctx, params, witness):
-        ctx._proved((2 * params.rounds + 2) // self.nranks)
+        # a rank proves with exactly the per-rank tables the one-GPU rehearsal times
+        # (tools/shard_rehearsal.py: prepare_shard(w, rank, N, distributed_h=True)), never the
+        # full-vector tables of bh_params_prepare
+        want = ("shard", self.rank, self.nranks, True)
+        assert params.prepared == want, f"rank {self.rank} prepared {params.prepared}, expected {want}"
+        ctx._proved((2 * params.rounds + 2) // self.nranks, params.table_bytes())
         return _h("partial", params.rounds, self.rank, n=PARTIAL_BYTES)
 
     def allgather(self, partial):

@@ -53,9 +53,27 @@ def test_bench_multirank_line(tmp_path, world):
     assert len(d["per_rank_ms_per_step"]) == world
     assert d["ms_per_step"] >= max(d["per_rank_ms_per_step"]) * 0.999  # max over ranks
     assert d["srs_window_tables"]["used"] == [5] * world
+    # every rank built only its own table slices (bh_params_prepare_shard), as rehearsed
+    assert d["srs_window_tables"]["prepare"] == ["shard"] * world
+    assert all(abs(gb - 31.4 / world) < 0.01 for gb in d["srs_window_tables"]["GB"])
     assert d["config"]["parallelism"] == f"msm-shard{world}" and d["config"]["exchange"] == "rccl"
     assert d["c5"]["proofs"] == 8 and d["c5"]["proofs_match_single"] is True
     assert d["value"] > 0 and d["proof_sha_prefix"]
+
+
+def test_bench_single_gpu_prepares_full_tables(tmp_path):
+    """N = 1: the full-vector tables (bh_params_prepare), reported as such."""
+    code = RUNNER.format(fakes=os.path.join(ROOT, "tests", "fakes"), bench=os.path.join(ROOT, "bench.py"))
+    env = dict(os.environ, FAKE_COMM_DIR=str(tmp_path), FAKE_DEVICES="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, "-c", code, "--log-constraints", "6", "--steps", "2", "--warmup", "1",
+                        "--cpu-baseline", "0", "--dropin", "0", "--c5", "0"], env=env, cwd=ROOT,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["srs_window_tables"]["prepare"] == "full"
+    assert abs(d["srs_window_tables"]["GB"] - 31.4) < 0.01
 
 
 def test_bench_rank_fails_on_missing_devices(tmp_path):

@@ -1,6 +1,7 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle's committed
 golden vectors and live oracle runs on the same seeded inputs.  Bit-exact for
 every integer/group result."""
+import hashlib
 import random
 
 import numpy as np
@@ -272,7 +273,12 @@ def test_window_tables_match_plain_windows(ctx, logc):
     parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, 2) for k in range(2))
     assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
     if logc == 22:
-        assert plain.hex().startswith("b320c6a265000d01babba804dc37ae10")
+        # the benchmark's own proof (C3) equals the oracle port's proof of the same CRS and
+        # witness, recorded in tests/golden/port_proofs.json by tools/cpu_baseline_full.py
+        # --fixture (prover.rs:315-349 output)
+        fx = _port_proof(22)
+        assert hashlib.sha256(params.write()).hexdigest() == fx["params_sha256"]
+        assert plain.hex() == fx["proof_port"]
 
 
 def test_checked_load_rejects_points_outside_subgroup(ctx):
@@ -292,6 +298,20 @@ def test_checked_load_rejects_points_outside_subgroup(ctx):
     # a valid subgroup point passes the checked path
     g = bytes.fromhex(_golden_first_g1())
     bh.Bases(ctx, bh.BH_G1, g, checked=True)
+
+
+def _port_proof(logc, required=True):
+    """tests/golden/port_proofs.json: the oracle C++ port's full-size proofs (MiMC chain, seed 7,
+    preimage seed 8, r = 27134, s = 17146) with the SHA-256 of the Parameters they were proved
+    with; written by tools/cpu_baseline_full.py --fixture on the GPU box."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "port_proofs.json")
+    fx = json.load(open(path)) if os.path.exists(path) else {}
+    if f"2^{logc}" not in fx:
+        assert not required, f"{path} has no 2^{logc} entry"
+        return None
+    return fx[f"2^{logc}"]
 
 
 def _golden_first_g1():
@@ -397,6 +417,15 @@ def test_c4_2p24_sharded_8_ways_equals_single_device_proof():
         params = bh.Parameters.chain(c, rounds)
         w = bh.Witness.chain(c, rounds)
         single = bh.prove_witness(c, params, w, 27134, 17146)
+        # the proof is valid (verify_proof, verifier.rs:23-62, natively) for the chain's image ...
+        public = bh.fr_from_mont(bh.chain_assignment(rounds)["inputs"])[1:]
+        vk = params.vk_bytes()
+        assert bh.verify_proof(vk, single, public)
+        assert not bh.verify_proof(vk, single, [(public[0] + 1) % R])
+        # ... and, where the oracle port has proved C4 (tests/golden/port_proofs.json), its proof
+        fx = _port_proof(24, required=False)
+        if fx is not None:
+            assert single.hex() == fx["proof_port"]
         params.prepare(w, 8)
         parts = b"".join(bh.prove_witness_partial(c, params, w, k, 8) for k in range(8))
         assert bh.proof_from_partials(params.vk_bytes(), parts, 8, 27134, 17146) == single
@@ -485,12 +514,14 @@ def test_fft_composition(ctx, logm):
         assert list(d.into_coeffs()) == v, (first, second)
 
 
-@pytest.mark.parametrize("rounds", [15, (1 << 15) - 1])
+@pytest.mark.parametrize("rounds", [15, 100, 5000, (1 << 15) - 1])
 def test_bh_prove_from_host_buffers(ctx, golden, rounds):
     """bh_prove, the drop-in entry point: the ProvingAssignment as
     host buffers in bls12_381's layouts (a/b/c/assignments as 4-limb Montgomery Fr, densities
     as bitvec words) straight to the 192-byte proof.  Equals the golden proof (r15) and the
-    device-resident-witness proof (2^16 constraints)."""
+    device-resident-witness proof (2^16 constraints).  100 and 5000 rounds give 202 and 10002
+    constraints, so the H block's domain (256, 16384) is zero-padded past the constraints (the
+    raw upload's padding branch); those proofs also verify natively."""
     bh = _bh()
     params = bh.Parameters.chain(ctx, rounds)
     asg = bh.chain_assignment(rounds)
@@ -500,6 +531,11 @@ def test_bh_prove_from_host_buffers(ctx, golden, rounds):
         assert proof.hex() == fx["proof"]
     assert proof == bh.prove_witness(ctx, params, bh.Witness.chain(ctx, rounds), 27134, 17146)
     assert bh.prove(ctx, params, asg, 27134, 17146) == proof  # buffers reused
+    if rounds in (100, 5000):
+        nc = asg["a"].shape[0]
+        assert nc & (nc - 1), "a constraint count that is not a power of two"
+        public = bh.fr_from_mont(asg["inputs"])[1:]
+        assert bh.verify_proof(params.vk_bytes(), proof, public)
 
 
 def test_async_multiexp_waiters_equal_sequential(ctx, golden):
@@ -532,6 +568,27 @@ def test_async_multiexp_waiters_equal_sequential(ctx, golden):
         with pytest.raises(bh.SynthesisError) as e:
             w.wait()
         assert e.value.code == case["error"]
+
+
+def test_async_multiexp_outlives_destroyed_context(golden):
+    """A Waiter whose context is destroyed before wait() is detached: wait() raises and touches
+    nothing of the context (bh_ctx_destroy used to free the slots outstanding jobs
+    pointed to).  A Waiter that goes out of scope unwaited is harmless too."""
+    bh = _bh()
+    c2 = bh.Context(0)
+    g1 = _bases(c2, bh.BH_G1, golden["msm_g1"]["bases"])
+    n = len(golden["msm_g1"]["bases"])
+    exps = [(7 ** (i + 3)) % R for i in range(n)]
+    want = bh.multiexp(c2, g1, 0, None, exps)
+    done = bh.multiexp_async(c2, g1, 0, None, exps)
+    assert done.wait() == want
+    pending = [bh.multiexp_async(c2, g1, 0, None, exps) for _ in range(3)]
+    dropped = bh.multiexp_async(c2, g1, 0, None, exps)
+    del dropped  # never waited: __del__ waits it (after which the context's slots stay intact)
+    c2.close()
+    for w in pending:
+        with pytest.raises(bh.SynthesisError):
+            w.wait()
 
 
 @pytest.mark.parametrize("logc,k,lanes", [(12, 5, 1), (12, 5, 2), (16, 6, 3), (20, 4, 2)])
