@@ -143,7 +143,12 @@ struct bh_ctx {
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
-  hipStream_t tstream[8] = {};     // prover: one reduction-tail stream per large multiexp (high priority)
+  // prover: reduction-tail streams (high priority, CU-masked on the first context of a device).
+  // A proof has at most 5 large multiexps unless the public inputs number in the thousands;
+  // more tails share these round robin.  Kept small for the device's hardware-queue budget
+  // (24 CP queues per MI355X, DESIGN.md section 5: a CU-masked stream owns a queue).
+  static constexpr int TAIL_STREAMS = 5;
+  hipStream_t tstream[TAIL_STREAMS] = {};
   bh::DistH* dist = nullptr;       // prover: this rank's distributed-H state (bh_prove_witness_partial_comm)
   int window_override = 0;
   int tables = 1;  // 1: the prover builds and uses SRS window tables (bh_ctx_set_tables)

@@ -21,8 +21,6 @@
 #include <stdint.h>
 #include "constants.h"
 
-#define BH_LIMB_BITS 29
-#define BH_LIMB_MASK 0x1fffffffu
 #define BH_DEV __device__ __forceinline__
 
 template <class C>
@@ -39,8 +37,8 @@ struct KP {
     uint64_t carry = 0;
     for (int i = 0; i < C::N; i++) {
       uint64_t t = (uint64_t)C::P[i] * K + carry;
-      l.v[i] = (uint32_t)(t & BH_LIMB_MASK);
-      carry = t >> BH_LIMB_BITS;
+      l.v[i] = (uint32_t)(t & C::MASK);
+      carry = t >> C::BITS;
     }
     return l;
   }
@@ -63,9 +61,102 @@ BH_DEV Fe<C> fe_one() {  // Montgomery form of 1
   return r;
 }
 
+// ---- Separated scans (configs with C::SEPARATED: 13 limbs of 30 bits for G1's Fp).  A column of
+// 30-bit limb products holds up to 13 terms < 2^60 (< 2^63.7), so the product and its Montgomery
+// reduction cannot share one 64-bit column accumulator as the 29-bit FIPS form does; they run as
+// two scans instead: t = a*b normalised to 2N limbs, then t + m*p column by column (t_k < 2^31
+// plus at most 13 terms m_i p_j).  13^2 + 13^2 = 338 v_mad_u64_u32 per product against 392 for
+// 14 x 29 bits, for one more normalisation (an and + shift per column).
+template <class C>
+BH_DEV Fe<C> fe_redc_sep(const uint32_t (&t)[2 * C::N]) {
+  constexpr int N = C::N;
+  Fe<C> r;
+  uint32_t m[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    acc += t[k];
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) acc += (uint64_t)m[i] * C::P[k - i];
+    if (k < N) {
+      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+      acc += (uint64_t)m[k] * C::P[0];
+    } else {
+      r.v[k - N] = (uint32_t)acc & C::MASK;
+    }
+    acc >>= C::BITS;
+  }
+  r.v[N - 1] = (uint32_t)acc + t[2 * N - 1];
+  return r;
+}
+
+template <class C>
+BH_DEV Fe<C> fe_mul_sep(const Fe<C>& a, const Fe<C>& b) {
+  constexpr int N = C::N;
+  static_assert(N * ((1ull << (2 * C::BITS)) >> 32) < (1ull << 32), "a product column must fit 64 bits");
+  uint32_t t[2 * N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) acc += (uint64_t)a.v[i] * b.v[k - i];
+    t[k] = (uint32_t)acc & C::MASK;
+    acc >>= C::BITS;
+  }
+  t[2 * N - 1] = (uint32_t)acc;
+  return fe_redc_sep<C>(t);
+}
+
+// (a*b + c*d) R^-1: the two product scans side by side (a column of both would overflow), their
+// limbs summed (< 2^31) into one reduction
+template <class C>
+BH_DEV Fe<C> fe_mul2_sep(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+  constexpr int N = C::N;
+  uint32_t t[2 * N];
+  uint64_t acc = 0, acd = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+      acc += (uint64_t)a.v[i] * b.v[k - i];
+      acd += (uint64_t)c.v[i] * d.v[k - i];
+    }
+    t[k] = ((uint32_t)acc & C::MASK) + ((uint32_t)acd & C::MASK);
+    acc >>= C::BITS;
+    acd >>= C::BITS;
+  }
+  t[2 * N - 1] = (uint32_t)acc + (uint32_t)acd;
+  return fe_redc_sep<C>(t);
+}
+
+// square: cross products once against 2a (limbs < 2^31: at most 6 cross terms < 2^61 and one
+// square < 2^60 per column)
+template <class C>
+BH_DEV Fe<C> fe_sqr_sep(const Fe<C>& a) {
+  constexpr int N = C::N;
+  uint32_t t[2 * N], a2[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) a2[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+      const int j = k - i;
+      if (i < j) acc += (uint64_t)a.v[i] * a2[j];
+      else if (i == j) acc += (uint64_t)a.v[i] * a.v[i];
+    }
+    t[k] = (uint32_t)acc & C::MASK;
+    acc >>= C::BITS;
+  }
+  t[2 * N - 1] = (uint32_t)acc;
+  return fe_redc_sep<C>(t);
+}
+
 // Montgomery product, FIPS column order. Output < 2p (see header).
 template <class C>
 BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
+  if constexpr (C::SEPARATED) return fe_mul_sep<C>(a, b);
   constexpr int N = C::N;
   Fe<C> r;
   uint32_t m[N];
@@ -79,12 +170,12 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
       acc += (uint64_t)m[i] * C::P[k - i];
     if (k < N) {
-      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
       acc += (uint64_t)m[k] * C::P[0];
     } else {
-      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+      r.v[k - N] = (uint32_t)acc & C::MASK;
     }
-    acc >>= BH_LIMB_BITS;
+    acc >>= C::BITS;
   }
   r.v[N - 1] = (uint32_t)acc;
   return r;
@@ -96,6 +187,7 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
 // operand bounds (in multiples of p) satisfy A*B + C*D < R/p (2^25 for DFp).
 template <class C>
 BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
+  if constexpr (C::SEPARATED) return fe_mul2_sep<C>(a, b, c, d);
   constexpr int N = C::N;
   static_assert(3 * N < 64, "3N products < 2^58 plus the carry must fit the 64-bit column accumulator");
   Fe<C> r;
@@ -112,12 +204,12 @@ BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
       acc += (uint64_t)m[i] * C::P[k - i];
     if (k < N) {
-      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
       acc += (uint64_t)m[k] * C::P[0];
     } else {
-      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+      r.v[k - N] = (uint32_t)acc & C::MASK;
     }
-    acc >>= BH_LIMB_BITS;
+    acc >>= C::BITS;
   }
   r.v[N - 1] = (uint32_t)acc;
   return r;
@@ -126,6 +218,7 @@ BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>
 // Montgomery square: cross products computed once against 2*a (limbs < 2^30).
 template <class C>
 BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
+  if constexpr (C::SEPARATED) return fe_sqr_sep<C>(a);
   constexpr int N = C::N;
   Fe<C> r;
   uint32_t m[N], a2[N];
@@ -146,12 +239,12 @@ BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
       acc += (uint64_t)m[i] * C::P[k - i];
     if (k < N) {
-      m[k] = ((uint32_t)acc * C::INV) & BH_LIMB_MASK;
+      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
       acc += (uint64_t)m[k] * C::P[0];
     } else {
-      r.v[k - N] = (uint32_t)acc & BH_LIMB_MASK;
+      r.v[k - N] = (uint32_t)acc & C::MASK;
     }
-    acc >>= BH_LIMB_BITS;
+    acc >>= C::BITS;
   }
   r.v[N - 1] = (uint32_t)acc;
   return r;
@@ -165,8 +258,8 @@ BH_DEV Fe<C> fe_add(const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
     uint32_t s = a.v[i] + b.v[i] + c;
-    r.v[i] = s & BH_LIMB_MASK;
-    c = s >> BH_LIMB_BITS;
+    r.v[i] = s & C::MASK;
+    c = s >> C::BITS;
   }
   return r;
 }
@@ -179,8 +272,8 @@ BH_DEV Fe<C> fe_sub(const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
     int32_t s = (int32_t)(a.v[i] + KP<C, K>::value.v[i]) - (int32_t)b.v[i] + c;
-    r.v[i] = (uint32_t)s & BH_LIMB_MASK;
-    c = s >> BH_LIMB_BITS;  // arithmetic shift: -1, 0 or +1
+    r.v[i] = (uint32_t)s & C::MASK;
+    c = s >> C::BITS;  // arithmetic shift: -1, 0 or +1
   }
   return r;
 }
@@ -199,8 +292,8 @@ BH_DEV Fe<C> fe_csub(const Fe<C>& x) {
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
     int32_t s = (int32_t)x.v[i] - (int32_t)KP<C, K>::value.v[i] + c;
-    t.v[i] = (uint32_t)s & BH_LIMB_MASK;
-    c = s >> BH_LIMB_BITS;
+    t.v[i] = (uint32_t)s & C::MASK;
+    c = s >> C::BITS;
   }
   const bool ge = (c >= 0);
   Fe<C> r;
@@ -226,15 +319,15 @@ BH_DEV Fe<C> fe_reduce_full(Fe<C> x) {
 // k = x0 * p^-1 mod 2^29 < 128 and the full comparison with k*p succeeds.
 template <class C>
 BH_DEV bool fe_is_zero(const Fe<C>& x) {
-  const uint32_t k = (x.v[0] * C::P0INV) & BH_LIMB_MASK;
+  const uint32_t k = (x.v[0] * C::P0INV) & C::MASK;
   if (k >= 128u) return false;
   uint64_t carry = 0;
   uint32_t diff = 0;
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
     uint64_t t = (uint64_t)C::P[i] * k + carry;
-    diff |= ((uint32_t)t & BH_LIMB_MASK) ^ x.v[i];
-    carry = t >> BH_LIMB_BITS;
+    diff |= ((uint32_t)t & C::MASK) ^ x.v[i];
+    carry = t >> C::BITS;
   }
   return diff == 0;
 }
@@ -261,6 +354,7 @@ BH_DEV Fe<C> fe_select(bool c, const Fe<C>& a, const Fe<C>& b) {
 template <class C> struct Packed;
 template <> struct Packed<FpCfg> { static constexpr int W = 12; };
 template <> struct Packed<FrCfg> { static constexpr int W = 8; };
+template <> struct Packed<Fp30Cfg> { static constexpr int W = 12; };
 
 template <class C>
 BH_DEV Fe<C> fe_unpack(const uint32_t* w) {
@@ -268,11 +362,11 @@ BH_DEV Fe<C> fe_unpack(const uint32_t* w) {
   Fe<C> r;
 #pragma unroll
   for (int i = 0; i < C::N; i++) {
-    const int bit = i * BH_LIMB_BITS;
+    const int bit = i * C::BITS;
     const int wi = bit >> 5, sh = bit & 31;
     uint64_t lo = w[wi];
     uint64_t hi = (wi + 1 < W) ? (uint64_t)w[wi + 1] : 0ull;
-    r.v[i] = (uint32_t)(((hi << 32) | lo) >> sh) & BH_LIMB_MASK;
+    r.v[i] = (uint32_t)(((hi << 32) | lo) >> sh) & C::MASK;
   }
   return r;
 }
@@ -287,8 +381,8 @@ BH_DEV void fe_pack(const Fe<C>& x, uint32_t* w) {
     const int bit0 = j * 32;
 #pragma unroll
     for (int i = 0; i < C::N; i++) {
-      const int b = i * BH_LIMB_BITS;
-      if (b + BH_LIMB_BITS <= bit0 || b >= bit0 + 32) continue;
+      const int b = i * C::BITS;
+      if (b + C::BITS <= bit0 || b >= bit0 + 32) continue;
       if (b >= bit0) acc |= (uint64_t)x.v[i] << (b - bit0);
       else acc |= (uint64_t)x.v[i] >> (bit0 - b);
     }
@@ -306,29 +400,34 @@ using DFr = Fe<FrCfg>;
 
 // Field-generic wrappers so the curve code is written once for DFp (G1) and DFp2 (G2).
 // MB = bound (in multiples of p) of a product; is_zero valid below 128p.
-struct FpOps {
-  using T = DFp;
+template <class Cfg>
+struct FpOpsT {
+  using Cf = Cfg;
+  using T = Fe<Cfg>;
   static constexpr uint32_t MB = 2;
-  static BH_DEV T mul(const T& a, const T& b) { return fe_mul<FpCfg>(a, b); }
-  static BH_DEV T sqr(const T& a) { return fe_sqr<FpCfg>(a); }
-  static BH_DEV T add(const T& a, const T& b) { return fe_add<FpCfg>(a, b); }
-  template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) { return fe_sub<FpCfg, K>(a, b); }
+  static BH_DEV T mul(const T& a, const T& b) { return fe_mul<Cfg>(a, b); }
+  static BH_DEV T sqr(const T& a) { return fe_sqr<Cfg>(a); }
+  static BH_DEV T add(const T& a, const T& b) { return fe_add<Cfg>(a, b); }
+  template <uint32_t K> static BH_DEV T sub(const T& a, const T& b) { return fe_sub<Cfg, K>(a, b); }
   // a*b - c*d with c < K*p: one reduction for both products (fe_mul2 of a, b, K*p - c, d); < 2p
   template <uint32_t K> static BH_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
-    return fe_mul2<FpCfg>(a, b, fe_neg<FpCfg, K>(c), d);
+    return fe_mul2<Cfg>(a, b, fe_neg<Cfg, K>(c), d);
   }
-  static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a); }
-  static BH_DEV T zero() { return fe_zero<FpCfg>(); }
-  static BH_DEV T one() { return fe_one<FpCfg>(); }
-  static BH_DEV T reduce(const T& a) { return fe_reduce_full<FpCfg>(a); }
+  static BH_DEV bool is_zero(const T& a) { return fe_is_zero<Cfg>(a); }
+  static BH_DEV T zero() { return fe_zero<Cfg>(); }
+  static BH_DEV T one() { return fe_one<Cfg>(); }
+  static BH_DEV T reduce(const T& a) { return fe_reduce_full<Cfg>(a); }
   static BH_DEV T neg_canonical(const T& a) {  // p - a for a in [0,p], result in [0,p]
-    return fe_csub<FpCfg, 1>(fe_sub<FpCfg, 1>(fe_zero<FpCfg>(), a));
+    return fe_csub<Cfg, 1>(fe_sub<Cfg, 1>(fe_zero<Cfg>(), a));
   }
-  static BH_DEV T select(bool c, const T& a, const T& b) { return fe_select<FpCfg>(c, a, b); }
+  static BH_DEV T select(bool c, const T& a, const T& b) { return fe_select<Cfg>(c, a, b); }
   static constexpr int PACKED_WORDS = 12;
-  static BH_DEV T unpack(const uint32_t* w) { return fe_unpack<FpCfg>(w); }
-  static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<FpCfg>(a, w); }
+  static BH_DEV T unpack(const uint32_t* w) { return fe_unpack<Cfg>(w); }
+  static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<Cfg>(a, w); }
 };
+using FpOps = FpOpsT<FpCfg>;      // 14 x 29-bit limbs (G2's Fp2 components)
+using Fp30Ops = FpOpsT<Fp30Cfg>;  // 13 x 30-bit limbs, separated scans
+
 
 // Fp2 product a*b = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u with Karatsuba's three column sums
 // shared by both halves: per column t0 = sum a0 b0, t1 = sum a1 b1, t2 = sum (a0+a1)(b0+b1);
@@ -365,16 +464,16 @@ BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, cons
       acc1 += (uint64_t)m1[i] * C::P[k - i];
     }
     if (k < N) {
-      m0[k] = ((uint32_t)acc0 * C::INV) & BH_LIMB_MASK;
+      m0[k] = ((uint32_t)acc0 * C::INV) & C::MASK;
       acc0 += (int64_t)((uint64_t)m0[k] * C::P[0]);
-      m1[k] = ((uint32_t)acc1 * C::INV) & BH_LIMB_MASK;
+      m1[k] = ((uint32_t)acc1 * C::INV) & C::MASK;
       acc1 += (uint64_t)m1[k] * C::P[0];
     } else {
-      r0.v[k - N] = (uint32_t)acc0 & BH_LIMB_MASK;
-      r1.v[k - N] = (uint32_t)acc1 & BH_LIMB_MASK;
+      r0.v[k - N] = (uint32_t)acc0 & C::MASK;
+      r1.v[k - N] = (uint32_t)acc1 & C::MASK;
     }
-    acc0 >>= BH_LIMB_BITS;
-    acc1 >>= BH_LIMB_BITS;
+    acc0 >>= C::BITS;
+    acc1 >>= C::BITS;
   }
   r1.v[N - 1] = (uint32_t)acc1;
   // r0's top limb is the signed remainder; add p when it is negative
@@ -383,8 +482,8 @@ BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, cons
 #pragma unroll
   for (int i = 0; i < N - 1; i++) {
     const uint32_t s = r0.v[i] + (C::P[i] & neg) + c;
-    r0.v[i] = s & BH_LIMB_MASK;
-    c = s >> BH_LIMB_BITS;
+    r0.v[i] = s & C::MASK;
+    c = s >> C::BITS;
   }
   r0.v[N - 1] = (uint32_t)acc0 + (C::P[N - 1] & neg) + c;
 }

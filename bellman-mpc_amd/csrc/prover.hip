@@ -617,11 +617,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   //   stream4   : the H pipeline (after the first accumulation, or first when distributed);
   //   stream3   : density maps, then every multiexp's sort (memory-bound, runs ahead);
   //   stream2   : the small (public-input) multiexps, whole;
-  //   tstream[q]: the reduction tail of the q-th large multiexp.
+  //   tstream[q % 5]: the reduction tail of the q-th large multiexp.
   // Each multiexp has its own workspace, so the only dependencies are the events below.
   hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
   hipStream_t tails[8];
-  for (int q = 0; q < 8; q++) tails[q] = ctx->tstream[q];
+  for (int q = 0; q < 8; q++) tails[q] = ctx->tstream[q % bh_ctx::TAIL_STREAMS];
   static const bool serial = [] {  // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
     const char* e = getenv("BH_PROVER_SERIAL");
     return e && e[0] == '1';

@@ -47,10 +47,9 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU port on a bounded sample (rank 0)")
     ap.add_argument("--cpu-log-constraints", type=int, default=16)
     ap.add_argument("--cpu-1t-log-constraints", type=int, default=12, help="1-thread CPU sample (0: skip)")
-    ap.add_argument("--cpu-full", type=int, default=0,
-                    help="also time the CPU port once on the bench's own workload (2^22: ~1 min on 256 threads, "
-                         "~8 min on the GPU box's 16-thread share; the committed run is "
-                         "profiles/r03_cpu_baseline_2p22.json)")
+    ap.add_argument("--cpu-full", type=int, default=1,
+                    help="also time the CPU port once on the bench's own workload (2^22: ~25 s on the GPU box's "
+                         "16-thread share; 0: report the committed run profiles/r03_cpu_baseline_2p22.json)")
     ap.add_argument("--check", type=int, default=1, help="verify the proof bytes are identical every step")
     ap.add_argument("--tables", type=int, default=1, help="prover SRS window tables (bh_ctx_set_tables)")
     ap.add_argument("--c5", type=int, default=64,
