@@ -60,8 +60,35 @@ Fr fr_from_dev_packed(const uint32_t in[8]) {
 
 // ------------------------------------------------------------------ device point conversion
 // canonical packed coordinates -> device Montgomery packed; optional on-curve check
+// G1 (G1F, curve.cuh): the same in G1's representation
+__global__ void __launch_bounds__(256) k_points_to_dev_g1(uint32_t* pts, size_t n, int check, uint32_t* bad) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  using F = G1F;
+  F::T r2;
+#pragma unroll
+  for (int k = 0; k < F::Cf::N; k++) r2.v[k] = F::Cf::R2[k];
+  F::T c[2];
+  uint32_t nz = 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    uint32_t* w = pts + (i * 2 + k) * 12;
+#pragma unroll
+    for (int l = 0; l < 12; l++) nz |= w[l];
+    c[k] = F::reduce(F::mul(F::unpack(w), r2));
+    F::pack(c[k], w);
+  }
+  if (check && nz) {  // (0,0) encodes the identity (never on the curve), skip it
+    const F::T four = F::add(F::add(F::one(), F::one()), F::add(F::one(), F::one()));
+    const F::T lhs = F::sqr(c[1]);
+    const F::T rhs = F::add(F::mul(F::sqr(c[0]), c[0]), four);
+    if (!F::is_zero(F::template sub<8>(lhs, rhs))) atomicOr(bad, 1u);
+  }
+}
+
 template <bool G2>
 __global__ void __launch_bounds__(256) k_points_to_dev(uint32_t* pts, size_t n, int check, uint32_t* bad) {
+  static_assert(G2, "G1 points: k_points_to_dev_g1");
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr int NC = G2 ? 4 : 2;  // DFp coordinates per point
@@ -106,7 +133,7 @@ __global__ void __launch_bounds__(256) k_points_to_dev(uint32_t* pts, size_t n, 
 template <bool G2>
 __global__ void __launch_bounds__(256) k_subgroup_check(const uint32_t* pts, size_t n, uint32_t* bad) {
   using C = typename std::conditional<G2, G2Ops, G1Ops>::type;
-  using F = typename std::conditional<G2, Fp2Ops, FpOps>::type;
+  using F = typename std::conditional<G2, Fp2Ops, G1F>::type;
   constexpr int PW = F::PACKED_WORDS;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -160,7 +187,7 @@ bh_status srs_upload_affine(bh_ctx* ctx, int group, const void* host_pts, size_t
     BH_TRY_HIP(hipMemcpyAsync(out->pts.p, w.data(), n * words * 4, hipMemcpyHostToDevice, ctx->stream));
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (group == BH_G1)
-      hipLaunchKernelGGL(k_points_to_dev<false>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+      hipLaunchKernelGGL(k_points_to_dev_g1, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
                          0, (uint32_t*)nullptr);
     else
       hipLaunchKernelGGL(k_points_to_dev<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
@@ -218,7 +245,7 @@ bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n,
     BH_TRY_HIP(hipMemcpyAsync(out->pts.p, w.data(), n * words * 4, hipMemcpyHostToDevice, ctx->stream));
     unsigned blocks = (unsigned)((n + 255) / 256);
     if (group == BH_G1)
-      hipLaunchKernelGGL(k_points_to_dev<false>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
+      hipLaunchKernelGGL(k_points_to_dev_g1, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
                          checked, bad.as<uint32_t>());
     else
       hipLaunchKernelGGL(k_points_to_dev<true>, dim3(blocks), dim3(256), 0, ctx->stream, out->pts.as<uint32_t>(), n,
@@ -256,13 +283,35 @@ static inline Fp fp_from_dev_limbs(const uint32_t* limbs14) {
   return fp_from_dev_words(words);
 }
 
-static Jac<Fp> g1_from_xyzz(const XYZZ<FpOps>& p) {
-  return xyzz_to_jac(fp_from_dev_limbs(p.X.v), fp_from_dev_limbs(p.Y.v), fp_from_dev_limbs(p.ZZ.v),
-                     fp_from_dev_limbs(p.ZZZ.v));
+// G1 (G1F: 13 balanced 30-bit digits or 14 x 29-bit limbs, R = 2^(N*BITS)): a canonical
+// coordinate's limbs (C::reduce) -> packed words -> host
+Fp fp_from_dev_words_g1(const uint32_t* w) {
+  using Cf = G1F::Cf;
+  return fp_from_dev_words_r<Cf::N * Cf::BITS>(w);
+}
+Fp fp_from_dev_g1(const G1F::T& x) {
+  using Cf = G1F::Cf;
+  uint32_t words[12] = {0};
+  int64_t carry = 0;
+  for (int i = 0; i < Cf::N; i++) {  // (signed) digits -> unsigned BITS-bit limbs of the value in [0, p)
+    const int64_t s = (int64_t)x.v[i] + carry;
+    const uint32_t limb = (uint32_t)(s & (int64_t)Cf::MASK);
+    carry = s >> Cf::BITS;
+    const int bit = Cf::BITS * i;
+    const int wi = bit >> 5, sh = bit & 31;
+    const uint64_t v = (uint64_t)limb << sh;
+    words[wi] |= (uint32_t)v;
+    if (wi + 1 < 12) words[wi + 1] |= (uint32_t)(v >> 32);
+  }
+  return fp_from_dev_words_g1(words);
+}
+
+static Jac<Fp> g1_from_xyzz(const XYZZ<G1F>& p) {
+  return xyzz_to_jac(fp_from_dev_g1(p.X), fp_from_dev_g1(p.Y), fp_from_dev_g1(p.ZZ), fp_from_dev_g1(p.ZZZ));
 }
 // window sums -> the multiexp (Horner over the Wb windows, c doublings each; multiexp.rs:244-249),
 // or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction)
-Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, const MsmShape& sh) {
+Jac<Fp> combine_g1(const XYZZ<G1F>* ws, const MsmShape& sh) {
   const int shift = reduce_split_shift(sh, false);
   if (shift >= 0) {
     Jac<Fp> z = g1_from_xyzz(ws[1]);
@@ -714,7 +763,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
-  if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<FpOps>), hipHostMallocDefault) != hipSuccess ||
+  if (hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<G1F>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
       hipHostMalloc(&c->host_spans, 8 * MAX_SPAN_BLOCKS * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
@@ -822,7 +871,7 @@ bh_status bh_srs_get(const bh_srs* srs, size_t i, uint8_t* out) {
   BH_TRY_HIP(hipMemcpy(w, srs->pts.as<uint32_t>() + i * words, words * 4, hipMemcpyDeviceToHost));
   bool inf = std::find(srs->identity_idx.begin(), srs->identity_idx.end(), i) != srs->identity_idx.end();
   if (srs->group == BH_G1) {
-    AffinePt<Fp> a{fp_from_dev_words(w), fp_from_dev_words(w + 12), inf};
+    AffinePt<Fp> a{fp_from_dev_words_g1(w), fp_from_dev_words_g1(w + 12), inf};
     g1_to_uncompressed(a, out);
   } else {
     AffinePt<bh::Fp2> a{bh::Fp2{fp_from_dev_words(w), fp_from_dev_words(w + 12)},

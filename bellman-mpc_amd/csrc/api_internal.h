@@ -158,7 +158,7 @@ struct bh_ctx {
   // tails of different multiexps never share buffers (about 1 GB each at 2^22 points)
   bh::MsmWorkspace<G1Ops> pw1[6];
   bh::MsmWorkspace<G2Ops> pw2[2];
-  XYZZ<FpOps>* host_out1 = nullptr;   // pinned, 8 jobs x 128 windows (c >= 2)
+  XYZZ<G1F>* host_out1 = nullptr;     // pinned, 8 jobs x 128 windows (c >= 2)
   XYZZ<Fp2Ops>* host_out2 = nullptr;  // pinned, 2 jobs x 128 windows
   hipEvent_t jev[48] = {};
   std::map<int, std::unique_ptr<bh::Domain>> domains;
@@ -199,8 +199,11 @@ void ctx_sync_all(bh_ctx* ctx);
 void fr_to_dev_limbs(const Fr& x, uint32_t out[9]);
 void fr_to_dev_packed(const Fr& x, uint32_t out[8]);
 Fr fr_from_dev_packed(const uint32_t in[8]);
+// G1 device coordinates (C::reduce output, G1F's limb or balanced-digit form; packed words) -> host
+Fp fp_from_dev_g1(const G1F::T& x);
+Fp fp_from_dev_words_g1(const uint32_t* w);
 // combine per-window sums (host Horner, multiexp.rs:244-249)
-Jac<Fp> combine_g1(const XYZZ<FpOps>* ws, const MsmShape& sh);
+Jac<Fp> combine_g1(const XYZZ<G1F>* ws, const MsmShape& sh);
 Jac<Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh);
 // run one MSM whose scalars/index map are already on the device; returns result on host
 bh_status msm_g1_device(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, const uint32_t* d_scalars, size_t n,

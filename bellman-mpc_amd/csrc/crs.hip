@@ -18,7 +18,7 @@ namespace bh {
 template <class C>
 struct FieldOf;
 template <>
-struct FieldOf<G1Ops> { using F = FpOps; };
+struct FieldOf<G1Ops> { using F = G1F; };
 template <>
 struct FieldOf<G2Ops> { using F = Fp2Ops; };
 
@@ -63,11 +63,24 @@ __device__ DFp fp_inv(const DFp& x) {
   return r;
 }
 
+// the same exponentiation over any Fp representation of the FpOpsT / FpSOps interface
 template <class F>
-struct Inv;
-template <>
-struct Inv<FpOps> {
-  static __device__ DFp run(const DFp& x) { return fp_inv(x); }
+__device__ typename F::T fp_inv_ops(const typename F::T& x) {
+  constexpr uint32_t E[12] = {0xffffaaa9u, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
+                              0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+  typename F::T r = F::one();
+  for (int w = 11; w >= 0; w--) {
+    for (int b = 31; b >= 0; b--) {
+      r = F::sqr(r);
+      if ((E[w] >> b) & 1u) r = F::mul(r, x);
+    }
+  }
+  return r;
+}
+
+template <class F>
+struct Inv {  // Fp in any representation (G1F)
+  static __device__ typename F::T run(const typename F::T& x) { return fp_inv_ops<F>(x); }
 };
 template <>
 struct Inv<Fp2Ops> {

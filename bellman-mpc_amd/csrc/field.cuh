@@ -61,114 +61,24 @@ BH_DEV Fe<C> fe_one() {  // Montgomery form of 1
   return r;
 }
 
-// ---- Separated scans (configs with C::SEPARATED: 13 limbs of 30 bits for G1's Fp).  A column of
-// 30-bit limb products holds up to 13 terms < 2^60 (< 2^63.7), so the product and its Montgomery
-// reduction cannot share one 64-bit column accumulator as the 29-bit FIPS form does; they run as
-// two scans instead: t = a*b normalised to 2N limbs, then t + m*p column by column (t_k < 2^31
-// plus at most 13 terms m_i p_j).  13^2 + 13^2 = 338 v_mad_u64_u32 per product against 392 for
-// 14 x 29 bits, for one more normalisation (an and + shift per column).
-template <class C>
-BH_DEV Fe<C> fe_redc_sep(const uint32_t (&t)[2 * C::N]) {
-  constexpr int N = C::N;
-  Fe<C> r;
-  uint32_t m[N];
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-    acc += t[k];
-#pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) acc += (uint64_t)m[i] * C::P[k - i];
-    if (k < N) {
-      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
-      acc += (uint64_t)m[k] * C::P[0];
-    } else {
-      r.v[k - N] = (uint32_t)acc & C::MASK;
-    }
-    acc >>= C::BITS;
-  }
-  r.v[N - 1] = (uint32_t)acc + t[2 * N - 1];
-  return r;
-}
-
-template <class C>
-BH_DEV Fe<C> fe_mul_sep(const Fe<C>& a, const Fe<C>& b) {
-  constexpr int N = C::N;
-  static_assert(N * ((1ull << (2 * C::BITS)) >> 32) < (1ull << 32), "a product column must fit 64 bits");
-  uint32_t t[2 * N];
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-#pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) acc += (uint64_t)a.v[i] * b.v[k - i];
-    t[k] = (uint32_t)acc & C::MASK;
-    acc >>= C::BITS;
-  }
-  t[2 * N - 1] = (uint32_t)acc;
-  return fe_redc_sep<C>(t);
-}
-
-// (a*b + c*d) R^-1: the two product scans side by side (a column of both would overflow), their
-// limbs summed (< 2^31) into one reduction
-template <class C>
-BH_DEV Fe<C> fe_mul2_sep(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
-  constexpr int N = C::N;
-  uint32_t t[2 * N];
-  uint64_t acc = 0, acd = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-#pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acd += (uint64_t)c.v[i] * d.v[k - i];
-    }
-    t[k] = ((uint32_t)acc & C::MASK) + ((uint32_t)acd & C::MASK);
-    acc >>= C::BITS;
-    acd >>= C::BITS;
-  }
-  t[2 * N - 1] = (uint32_t)acc + (uint32_t)acd;
-  return fe_redc_sep<C>(t);
-}
-
-// square: cross products once against 2a (limbs < 2^31: at most 6 cross terms < 2^61 and one
-// square < 2^60 per column)
-template <class C>
-BH_DEV Fe<C> fe_sqr_sep(const Fe<C>& a) {
-  constexpr int N = C::N;
-  uint32_t t[2 * N], a2[N];
-#pragma unroll
-  for (int i = 0; i < N; i++) a2[i] = a.v[i] << 1;
-  uint64_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < 2 * N - 1; k++) {
-#pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-      const int j = k - i;
-      if (i < j) acc += (uint64_t)a.v[i] * a2[j];
-      else if (i == j) acc += (uint64_t)a.v[i] * a.v[i];
-    }
-    t[k] = (uint32_t)acc & C::MASK;
-    acc >>= C::BITS;
-  }
-  t[2 * N - 1] = (uint32_t)acc;
-  return fe_redc_sep<C>(t);
-}
-
 // Montgomery product, FIPS column order. Output < 2p (see header).
 template <class C>
 BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
-  if constexpr (C::SEPARATED) return fe_mul_sep<C>(a, b);
   constexpr int N = C::N;
   Fe<C> r;
   uint32_t m[N];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
+    // the column's a*b products and m*p products as two independent mad chains
+    uint64_t acc2 = 0;
 #pragma unroll
     for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
       acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
-      acc += (uint64_t)m[i] * C::P[k - i];
+      acc2 += (uint64_t)m[i] * C::P[k - i];
+    acc += acc2;
     if (k < N) {
       m[k] = ((uint32_t)acc * C::INV) & C::MASK;
       acc += (uint64_t)m[k] * C::P[0];
@@ -187,7 +97,6 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
 // operand bounds (in multiples of p) satisfy A*B + C*D < R/p (2^25 for DFp).
 template <class C>
 BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
-  if constexpr (C::SEPARATED) return fe_mul2_sep<C>(a, b, c, d);
   constexpr int N = C::N;
   static_assert(3 * N < 64, "3N products < 2^58 plus the carry must fit the 64-bit column accumulator");
   Fe<C> r;
@@ -218,7 +127,6 @@ BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>
 // Montgomery square: cross products computed once against 2*a (limbs < 2^30).
 template <class C>
 BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
-  if constexpr (C::SEPARATED) return fe_sqr_sep<C>(a);
   constexpr int N = C::N;
   Fe<C> r;
   uint32_t m[N], a2[N];
@@ -354,7 +262,6 @@ BH_DEV Fe<C> fe_select(bool c, const Fe<C>& a, const Fe<C>& b) {
 template <class C> struct Packed;
 template <> struct Packed<FpCfg> { static constexpr int W = 12; };
 template <> struct Packed<FrCfg> { static constexpr int W = 8; };
-template <> struct Packed<Fp30Cfg> { static constexpr int W = 12; };
 
 template <class C>
 BH_DEV Fe<C> fe_unpack(const uint32_t* w) {
@@ -425,8 +332,7 @@ struct FpOpsT {
   static BH_DEV T unpack(const uint32_t* w) { return fe_unpack<Cfg>(w); }
   static BH_DEV void pack(const T& a, uint32_t* w) { fe_pack<Cfg>(a, w); }
 };
-using FpOps = FpOpsT<FpCfg>;      // 14 x 29-bit limbs (G2's Fp2 components)
-using Fp30Ops = FpOpsT<Fp30Cfg>;  // 13 x 30-bit limbs, separated scans
+using FpOps = FpOpsT<FpCfg>;  // 14 x 29-bit limbs
 
 
 // Fp2 product a*b = (a0 b0 - a1 b1) + (a0 b1 + a1 b0) u with Karatsuba's three column sums

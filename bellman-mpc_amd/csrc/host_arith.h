@@ -338,6 +338,25 @@ static inline Fp fp_from_dev_words(const uint32_t* w) {
   }();
   return mul(a, K);
 }
+// Device packed words of a field whose device Montgomery radix is 2^rlog (G1's form, R = 2^(N*BITS)
+// of its limb configuration: 2^390 for the balanced 13 x 30-bit digits) -> host Montgomery:
+// a * 2^-(rlog - 384) = mont_mul(a, 2^(768 - rlog) mod p)
+template <int RLOG>
+static inline Fp fp_from_dev_words_r(const uint32_t* w) {
+  Fp a;
+  for (int i = 0; i < 6; i++) a.v[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+  static Fp K = [] {
+    uint64_t two[6] = {2, 0, 0, 0, 0, 0};
+    Fp t = from_int<6>(two);
+    uint64_t e[1] = {768 - RLOG};
+    Fp k = pow_vartime(t, e, 1);  // Montgomery(2^(768 - RLOG))
+    uint64_t raw[6];
+    to_int(k, raw);               // canonical
+    Fp out; memcpy(out.v, raw, sizeof raw);
+    return out;
+  }();
+  return mul(a, K);
+}
 // host Montgomery -> device packed words (x * 2^406 mod p)
 static inline void fp_to_dev_words(const Fp& x, uint32_t* w) {
   static Fp K = [] {

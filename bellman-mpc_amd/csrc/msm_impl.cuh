@@ -13,7 +13,7 @@ static inline unsigned msm_blocks_for(size_t n, unsigned bs) { return (unsigned)
 // ----------------------------------------------------------------- accumulate
 template <class C>
 __device__ __forceinline__ typename C::A load_base(const uint32_t* bases, uint32_t e, uint32_t rec) {
-  using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+  using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
   constexpr int PW = F::PACKED_WORDS;
   const uint32_t idx = e & 0x7fffffffu;
   const uint4* p = reinterpret_cast<const uint4*>(bases + (size_t)idx * rec);
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, 
                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
                                                        typename C::P* bucket_sums, typename C::P* conts,
                                                        uint32_t* cont_bucket) {
-  using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+  using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
   constexpr int PW = F::PACKED_WORDS;
   constexpr int NQ = 2 * PW / 4;  // 16-byte pieces per affine base
   __shared__ uint4 pre[4][NQ][64];
@@ -580,7 +580,7 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     const size_t Emax = n * (size_t)sh.W;
     const size_t segs = (Emax + sh.S - 1) / sh.S;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
-    using F = typename std::conditional<std::is_same<C, G1Ops>::value, FpOps, Fp2Ops>::type;
+    using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
     hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
                        ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,

@@ -77,7 +77,7 @@ void write_vec(const bh_srs& v, std::vector<uint8_t>& out) {
     const uint32_t* d = &w[i * words];
     uint8_t* o = &out[base + i * pb];
     if (v.group == BH_G1) {
-      g1_to_uncompressed(AffinePt<Fp>{fp_from_dev_words(d), fp_from_dev_words(d + 12), inf[i] != 0}, o);
+      g1_to_uncompressed(AffinePt<Fp>{fp_from_dev_words_g1(d), fp_from_dev_words_g1(d + 12), inf[i] != 0}, o);
     } else {
       g2_to_uncompressed(AffinePt<bh::Fp2>{bh::Fp2{fp_from_dev_words(d), fp_from_dev_words(d + 12)},
                                            bh::Fp2{fp_from_dev_words(d + 24), fp_from_dev_words(d + 36)}, inf[i] != 0},

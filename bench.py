@@ -10,7 +10,7 @@ the complete assignment already resident in HBM; the output is the 192-byte
 proof.  Synthesis and CRS generation are outside the timed region.
 
 Multi-GPU (`--gpus N`, launched by torch.distributed.run): every MSM is
-sharded by scalar/point range over the N ranks; for N >= 4 (power of two) the H
+sharded by scalar/point range over the N ranks; for N >= 2 (power of two) the H
 block is distributed too (three RCCL all-to-alls per proof, dist_h.h) and each
 rank's h multiexp covers the coefficients it ends with.  Each rank returns its 8
 partial sums, RCCL all-gathers them and rank 0 adds them and assembles the
@@ -283,7 +283,7 @@ def main():
     def step():
         if world == 1:
             return bh.prove_witness(ctx, params, witness, r, s)
-        # this rank's share of every multiexp (H block distributed over RCCL for N >= 4),
+        # this rank's share of every multiexp (H block distributed over RCCL for N >= 2),
         # the 960-byte partial records all-gathered over RCCL, rank 0 sums and assembles
         parts = comm.allgather(comm.prove_partial(ctx, params, witness))
         if rank == 0:

@@ -4,12 +4,14 @@
 // both representations from canonical inputs and compares the canonical outputs word for word;
 // part 2 times chains of mixed additions (curvebench's shape) and of plain products.
 #include "../../bellman-mpc_amd/csrc/curve.cuh"
+#include "fp_variants.cuh"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 using G1_29 = CurveOps<FpOps>;
 using G1_30 = CurveOps<Fp30Ops>;
+using G1_30s = CurveOps<Fp30sOps>;
 
 template <class F>
 __device__ typename F::T to_mont(const uint32_t* w) {
@@ -72,7 +74,7 @@ __global__ void __launch_bounds__(256, W) kmadd(const uint32_t* pts, uint32_t* o
 }
 
 template <class F>
-__global__ void __launch_bounds__(256, 2) kmul(uint32_t* x, int iters) {
+__global__ void __launch_bounds__(256, 2) kmul(const uint32_t* x, uint32_t* out, int iters) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   typename F::T a = F::unpack(x + (t & 1023) * 12), b = F::unpack(x + ((t + 1) & 1023) * 12);
   typename F::T c = F::unpack(x + ((t + 2) & 1023) * 12), d = F::unpack(x + ((t + 3) & 1023) * 12);
@@ -80,7 +82,7 @@ __global__ void __launch_bounds__(256, 2) kmul(uint32_t* x, int iters) {
     a = F::mul(a, b);
     c = F::mul(c, d);
   }
-  F::pack(F::add(a, c), x + 1024 * 12 + t * 12);
+  F::pack(F::add(a, c), out + (size_t)t * 12);  // out holds >= 12 words per thread
 }
 
 static const char* P_HEX = "1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab";
@@ -95,13 +97,15 @@ int main() {
     h_in[i] = (uint32_t)s;
     if (i % 12 == 11) h_in[i] &= 0x19ffffffu;  // < p's top word 0x1a0111ea
   }
-  uint32_t *d_in, *o29, *o30;
+  uint32_t *d_in, *o29, *o30, *o30s;
   hipMalloc(&d_in, (size_t)n * 8 * 12 * 4);
   hipMalloc(&o29, (size_t)n * 7 * 12 * 4);
   hipMalloc(&o30, (size_t)n * 7 * 12 * 4);
+  hipMalloc(&o30s, (size_t)n * 7 * 12 * 4);
   hipMemcpy(d_in, h_in, (size_t)n * 8 * 12 * 4, hipMemcpyHostToDevice);
   kcheck<G1_29, FpOps><<<n / 256, 256>>>(d_in, o29, n);
   kcheck<G1_30, Fp30Ops><<<n / 256, 256>>>(d_in, o30, n);
+  kcheck<G1_30s, Fp30sOps><<<n / 256, 256>>>(d_in, o30s, n);
   hipDeviceSynchronize();
   uint32_t* a = (uint32_t*)malloc((size_t)n * 7 * 12 * 4);
   uint32_t* b = (uint32_t*)malloc((size_t)n * 7 * 12 * 4);
@@ -110,11 +114,16 @@ int main() {
   long bad = 0;
   for (size_t i = 0; i < (size_t)n * 7 * 12; i++) bad += a[i] != b[i];
   printf("cross-check (%d threads x 7 results, 29-bit vs 30-bit limbs): %ld differing words\n", n, bad);
+  hipMemcpy(b, o30s, (size_t)n * 7 * 12 * 4, hipMemcpyDeviceToHost);
+  long bad_s = 0;
+  for (size_t i = 0; i < (size_t)n * 7 * 12; i++) bad_s += a[i] != b[i];
+  printf("cross-check (29-bit vs 30-bit balanced digits): %ld differing words\n", bad_s);
+  bad += bad_s;
   (void)P_HEX;
 
   uint32_t *pts, *out;
   hipMalloc(&pts, 4096 * 48 * 4);
-  hipMalloc(&out, (size_t)(1 << 21) * 48 * 4);
+  hipMalloc(&out, (size_t)(1 << 21) * 48 * 4);  // >= 48 words per thread of the 2^20-thread grids
   hipMemcpy(pts, d_in, 4096 * 24 * 4, hipMemcpyDeviceToDevice);  // canonical values as bases
   hipMemcpy(pts + 4096 * 24, d_in, 4096 * 24 * 4, hipMemcpyDeviceToDevice);
   hipEvent_t e0, e1;
@@ -134,7 +143,7 @@ int main() {
   printf("%s W=%d: %.2f G madd/s (%.2f ms)\n", name, W, nthr* iters / (ms * 1e6), ms);
 #define RUNMUL(F, name)                                                                                     \
   hipEventRecord(e0);                                                                                       \
-  kmul<F><<<blocks, threads>>>(pts, 256);                                                                   \
+  kmul<F><<<blocks, threads>>>(pts, out, 256);                                                                   \
   hipEventRecord(e1);                                                                                       \
   hipEventSynchronize(e1);                                                                                  \
   hipEventElapsedTime(&ms, e0, e1);                                                                         \
@@ -142,7 +151,8 @@ int main() {
   for (int r = 0; r < 2; r++) {
     RUN(G1_29, FpOps, 1, "G1 14x29") RUN(G1_29, FpOps, 2, "G1 14x29")
     RUN(G1_30, Fp30Ops, 1, "G1 13x30") RUN(G1_30, Fp30Ops, 2, "G1 13x30")
-    RUNMUL(FpOps, "mul 14x29") RUNMUL(Fp30Ops, "mul 13x30")
+    RUN(G1_30s, Fp30sOps, 1, "G1 13x30s") RUN(G1_30s, Fp30sOps, 2, "G1 13x30s")
+    RUNMUL(FpOps, "mul 14x29") RUNMUL(Fp30Ops, "mul 13x30") RUNMUL(Fp30sOps, "mul 13x30s")
   }
   printf("err=%s\n", hipGetErrorString(hipGetLastError()));
   return bad == 0 ? 0 : 1;

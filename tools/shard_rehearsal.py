@@ -3,8 +3,8 @@
 
 For each N and rank k (default: 0 and N-1): the rank's Parameters are prepared exactly as a
 rank process of an N-GPU run holds them (bh_params_prepare_shard: its window-table slices
-and, for N >= 4, its gathered share of the h vector), then bh_rehearse_rank runs that rank's
-whole device work -- its 1/N of every multiexp and, for N >= 4, its part of the distributed
+and, for N >= 2, its gathered share of the h vector), then bh_rehearse_rank runs that rank's
+whole device work -- its 1/N of every multiexp and, for N >= 2, its part of the distributed
 H block, each all-to-all moving only the rank's own chunks (the xGMI transfer itself, ~2 MB
 per link per all-to-all at 2^22 and N = 8, is not included; neither are the 960-byte
 all-gather and rank 0's host combine, ~0.5 ms).  Predicted speed-up = t(1) / max_k t_k(N).
@@ -42,7 +42,7 @@ def main():
         per, setup, tabs = {}, {}, {}
         for k in ks:
             t0 = time.perf_counter()
-            params.prepare_shard(w, k, n)  # this rank's slices only (and its h share for N >= 4)
+            params.prepare_shard(w, k, n)  # this rank's slices only (and its h share for N >= 2)
             setup[k] = round(time.perf_counter() - t0, 3)
             bh.rehearse_rank(ctx, params, w, k, n)  # warm-up
             ts = [bh.rehearse_rank(ctx, params, w, k, n) for _ in range(args.reps)]
