@@ -469,7 +469,7 @@ static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const F
 }
 
 void ctx_sync_all(bh_ctx* ctx) {
-  for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4})
+  for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d})
     if (st) (void)hipStreamSynchronize(st);
   for (hipStream_t st : ctx->tstream)
     if (st) (void)hipStreamSynchronize(st);
@@ -731,11 +731,11 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   c->cu_masked = device >= 0 && device < 64 && g_masked_ctxs[device].fetch_add(1) == 0;
   if (!c->cu_masked && device >= 0 && device < 64) g_masked_ctxs[device].fetch_sub(1);
-  auto masked = [&](const char* var, hipStream_t* st) -> int {  // 1 created, 0 not asked, -1 error
+  // 1 created, 0 not asked, -1 error; def_k: the CUs the stream gets unless `var` says otherwise
+  auto masked = [&](const char* var, hipStream_t* st, int def_k) -> int {
     if (!c->cu_masked) return 0;
     const char* e = getenv(var);
-    const bool tails = strcmp(var, "BH_TAIL_CUS") == 0;
-    const int k = e ? atoi(e) : (tails ? ncu / 4 : 0);
+    const int k = e ? atoi(e) : def_k;
     if (k <= 0 || ncu <= 0 || k >= ncu) return 0;
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     const int step = ncu / k;
@@ -744,7 +744,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess ? 1 : -1;
   };
   for (auto& t : c->tstream) {
-    const int r = masked("BH_TAIL_CUS", &t);
+    const int r = masked("BH_TAIL_CUS", &t, ncu / 4);
     if (r < 0 || (r == 0 && hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess)) {
       release_mask(c); delete c;
       return BH_ERR_HIP;
@@ -752,13 +752,18 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   }
   for (hipStream_t* sp : {&c->stream3, &c->stream4}) {
     hipStream_t m = nullptr;
-    const int r = masked(sp == &c->stream3 ? "BH_SORT_CUS" : "BH_H_CUS", &m);
+    const int r = masked(sp == &c->stream3 ? "BH_SORT_CUS" : "BH_H_CUS", &m, 0);
     if (r < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
     if (r > 0) {
       (void)hipStreamDestroy(*sp);
       *sp = m;
     }
   }
+  // The distributed H block (N >= 2 ranks) on half the CUs: its passes, all-to-alls and DFTs then
+  // leave the other half to the accumulations instead of taking every CU as their waves retire
+  // (N = 8 rehearsal: 10.88 -> 10.54 ms per rank; 64 or 192 CUs, or the sorts masked too, were
+  // no better: profiles/r03_ab_rehearsal_*).  Replicated H (one GPU) keeps the unmasked stream4.
+  if (masked("BH_DIST_H_CUS", &c->stream4d, ncu / 2) < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
@@ -804,6 +809,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   (void)hipStreamDestroy(ctx->stream2);
   (void)hipStreamDestroy(ctx->stream3);
   (void)hipStreamDestroy(ctx->stream4);
+  if (ctx->stream4d) (void)hipStreamDestroy(ctx->stream4d);
   for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
   release_mask(ctx);
   delete ctx->dist;

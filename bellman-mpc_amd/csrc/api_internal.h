@@ -117,6 +117,11 @@ struct bh_params {
   // h bases of one rank's distributed-H share (dist_h.h: h[M*t + q], q in the rank's chunk),
   // gathered into share order so that a shard-sized window table covers them; key (N, rank, L)
   std::map<std::tuple<int, int, int>, std::unique_ptr<bh_srs>> h_shares;
+  // host copies of the leading bases of a, b_g1, b_g2 (the public inputs' bases), read back from
+  // the device on first use (under mu, exclusively) for the host input multiexps
+  std::mutex head_mu;
+  std::vector<bh::AffinePt<bh::Fp>> h_a_head, h_b1_head;
+  std::vector<bh::AffinePt<bh::Fp2>> h_b2_head;
 };
 
 struct bh_witness {
@@ -134,6 +139,9 @@ struct bh_witness {
   // raw = true: abc/inputs/aux hold the caller's bls12_381 Montgomery words, not yet converted
   // (bh_prove's asynchronous upload; the prover converts on its own streams)
   bool raw = false;
+  // the public inputs as canonical scalars on the host too (4 LE u64 each): the input
+  // multiexps of a proof are a handful of terms and run on a host thread (prover.hip)
+  std::vector<uint64_t> h_inputs;
 };
 
 struct bh_ctx {
@@ -143,6 +151,7 @@ struct bh_ctx {
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
+  hipStream_t stream4d = nullptr; // prover: the distributed H pipeline, CU-masked (first context of a device)
   // prover: reduction-tail streams (high priority, CU-masked on the first context of a device).
   // A proof has at most 5 large multiexps unless the public inputs number in the thousands;
   // more tails share these round robin.  Kept small for the device's hardware-queue budget

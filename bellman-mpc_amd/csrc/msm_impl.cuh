@@ -607,7 +607,10 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   // continuation partials: a bucket spanning up to REDUCE_FOLD_SPAN segments has them added
   // by its reduction thread (no extra launch); longer spans (known from the sort) are folded
   // first -- Q threads per bucket, or log-depth 4-ary tree levels
-  constexpr int REDUCE_FOLD_SPAN = 8;
+  static const size_t REDUCE_FOLD_SPAN = [] {  // BH_FOLD_SPAN: A/B experiments
+    const char* e = getenv("BH_FOLD_SPAN");
+    return e ? (size_t)atol(e) : (size_t)8;
+  }();
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
   const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;

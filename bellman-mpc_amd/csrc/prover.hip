@@ -125,6 +125,12 @@ bh_status witness_host(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint
     for (size_t k = 0; k < words; k++) pc[k + 1] = pc[k] + (size_t)__builtin_popcountll(d[k]);
     return pc;
   };
+  w->h_inputs.resize(ni * 4);
+  for (size_t i = 0; i < ni; i++) {  // bls12_381 Montgomery -> canonical
+    Fr x;
+    memcpy(x.v, inputs + 4 * i, 32);
+    fr_to_canonical(x, &w->h_inputs[4 * i]);
+  }
   w->a_aux_prefix = prefix(w->a_aux_density, w->a_aux_words);
   w->b_aux_prefix = prefix(w->b_aux_density, w->b_aux_words);
   w->a_aux_total = popcount_words(w->a_aux_density, na);
@@ -432,6 +438,65 @@ bh_status ensure_h_share(bh_ctx* ctx, bh_params* params, const ShareGeom& g, bh_
   return BH_OK;
 }
 
+// ---- The public-input multiexps (a_inputs, b_g1_inputs, b_g2_inputs: prover.rs:262-307 over
+// the input assignment) are a few terms for any circuit with few public inputs -- 2 for the
+// MiMC chain, at most 1 per rank of an N-GPU run.  On the device each would still run a full
+// sort and bucket reduction on the side streams, beside the accumulations; a host thread
+// computes them (double-and-add, bellman's own per-term cost) while the device works.
+constexpr size_t HOST_INPUT_MSM_MAX = 64;
+
+// the first n points of a device vector, on the host (device Montgomery -> host Montgomery)
+template <bool G2>
+bh_status read_head(const bh_srs& v, size_t n, std::vector<typename std::conditional<G2, AffinePt<bh::Fp2>, AffinePt<Fp>>::type>* out) {
+  const size_t words = G2 ? 48 : 24;
+  std::vector<uint32_t> w(std::max<size_t>(n, 1) * words);
+  if (n) BH_TRY_HIP(hipMemcpy(w.data(), v.pts.p, n * words * 4, hipMemcpyDeviceToHost));
+  out->resize(n);
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t* d = &w[i * words];
+    if constexpr (G2)
+      (*out)[i] = AffinePt<bh::Fp2>{bh::Fp2{fp_from_dev_words(d), fp_from_dev_words(d + 12)},
+                                    bh::Fp2{fp_from_dev_words(d + 24), fp_from_dev_words(d + 36)}, false};
+    else
+      (*out)[i] = AffinePt<Fp>{fp_from_dev_words_g1(d), fp_from_dev_words_g1(d + 12), false};
+  }
+  return BH_OK;
+}
+
+// shard [lo, hi) of the input multiexps -> r_a (a_inputs), r_b1 (b_g1_inputs), r_b2 (b_g2_inputs)
+bh_status host_input_msms(int device, bh_params* p, const bh_witness* w, size_t lo, size_t hi, Jac<Fp>* r_a,
+                          Jac<Fp>* r_b1, Jac<bh::Fp2>* r_b2) {
+  *r_a = jac_identity<Fp>();
+  *r_b1 = jac_identity<Fp>();
+  *r_b2 = jac_identity<bh::Fp2>();
+  if (hi <= lo) return BH_OK;
+  const auto bit = [&](size_t i) { return (w->b_input_density[i / 64] >> (i % 64)) & 1ull; };
+  size_t nb = 0;  // b bases consumed before lo, and the total up to hi
+  for (size_t i = 0; i < lo; i++) nb += bit(i);
+  size_t nb_hi = nb;
+  for (size_t i = lo; i < hi; i++) nb_hi += bit(i);
+  {
+    std::lock_guard<std::mutex> lk(p->head_mu);
+    if (p->h_a_head.size() < hi || p->h_b1_head.size() < nb_hi) {
+      if (hipSetDevice(device) != hipSuccess) return BH_ERR_HIP;
+      bh_status s;
+      if ((s = read_head<false>(p->a, hi, &p->h_a_head))) return s;
+      if ((s = read_head<false>(p->b_g1, nb_hi, &p->h_b1_head))) return s;
+      if ((s = read_head<true>(p->b_g2, nb_hi, &p->h_b2_head))) return s;
+    }
+  }
+  for (size_t i = lo; i < hi; i++) {
+    const uint64_t* k = &w->h_inputs[4 * i];
+    *r_a = jac_add(*r_a, jac_mul(jac_from_affine(p->h_a_head[i]), k, 4));
+    if (bit(i)) {
+      *r_b1 = jac_add(*r_b1, jac_mul(jac_from_affine(p->h_b1_head[nb]), k, 4));
+      *r_b2 = jac_add(*r_b2, jac_mul(jac_from_affine(p->h_b2_head[nb]), k, 4));
+      nb++;
+    }
+  }
+  return BH_OK;
+}
+
 // Caller holds params->mu: exclusively with build = true (tables and shares are rebuilt in
 // place), shared otherwise.
 // Plan the 8 multiexps of shard `shard` of `nshards`: scalar ranges, the base ranges they
@@ -651,6 +716,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ShareGeom geom;
   if (dh) {
     geom.N = dh->N; geom.rank = dh->rank; geom.L = L; geom.M = dh->M; geom.C = dh->C;
+    if (ctx->stream4d && !serial) sH = ctx->stream4d;  // on half the CUs (bh_ctx_create)
   }
   const ShareGeom* sg = dh ? &geom : nullptr;
   const uint32_t* sh_buf = dh ? dh->hbuf.as<uint32_t>() : nullptr;
@@ -675,6 +741,24 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                         jobs)))
       return s;
   }
+  // the public-input multiexps on a host thread (HOST_INPUT_MSM_MAX); BH_HOST_INPUTS=0: on the
+  // device like the others (A/B experiments)
+  static const bool host_inputs_on = [] {
+    const char* e = getenv("BH_HOST_INPUTS");
+    return !(e && e[0] == '0');
+  }();
+  const bool host_in = host_inputs_on && jobs[5].hi - jobs[5].lo <= HOST_INPUT_MSM_MAX;
+  struct HostInputs {
+    std::thread th;
+    bh_status st = BH_OK;
+    Jac<Fp> a, b1;
+    Jac<bh::Fp2> b2;
+    ~HostInputs() { if (th.joinable()) th.join(); }
+  } hin;
+  if (host_in)
+    hin.th = std::thread([&hin, ctx, mparams, w, lo = jobs[5].lo, hi = jobs[5].hi] {
+      hin.st = host_input_msms(ctx->device, mparams, w, lo, hi, &hin.a, &hin.b1, &hin.b2);
+    });
   if (up) {  // witness still uploading (bh_prove): density maps, inputs and aux first
     if (!up->wait(1)) return up->status;
     BH_TRY_HIP(hipStreamWaitEvent(sS, up->ev[0], 0));
@@ -877,7 +961,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   int big[8], nbig = 0, small[8], nsmall = 0;
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];
-    if (!n) continue;
+    if (!n || (host_in && j >= 5)) continue;
     if (n < SMALL_JOB && !jobs[j].is_h) small[nsmall++] = j;
     else big[nbig++] = j;
   }
@@ -902,6 +986,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       while (L > 1 && (size_t)sl.Wb * (size_t)(sl.NB / L) < (size_t)last_threads) L >>= 1;
       sl.L = L;
     }
+    // BH_LAST_ACC_ROUNDS = r (A/B experiments): the last accumulation in r resident rounds instead
+    // of fit_segments' 4 (longer segments: fewer continuation partials for its tail to fold)
+    static const int last_rounds = [] {
+      const char* e = getenv("BH_LAST_ACC_ROUNDS");
+      return e ? atoi(e) : 0;
+    }();
+    if (last_rounds > 0 && last_rounds < 4) sl.S = std::min(sl.S * 4 / last_rounds, 1 << 16);
   }
   // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it;
   // 1 = from the start, concurrent with everything; 2 = after the first accumulation (the
@@ -1009,6 +1100,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(hipStreamSynchronize(sA));
   BH_TRY_HIP(hipStreamSynchronize(sH));
   BH_TRY_HIP(hipStreamSynchronize(sT));
+  if (host_in) {
+    hin.th.join();
+    if (hin.st) return hin.st;
+    res1[jobs[5].out] = hin.a;
+    res1[jobs[6].out] = hin.b1;
+    res2[jobs[7].out] = hin.b2;
+  }
   const auto t_gpu = std::chrono::steady_clock::now();
 
   const auto t1 = std::chrono::steady_clock::now();
