@@ -1003,11 +1003,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     return e ? atoi(e) : -1;
   }();
   // 3 = concurrent with everything like 1, but enqueued by the host after the first
-  // accumulation (enqueueing H's passes and all-to-alls takes the host ~0.4 ms that the first
-  // sort would otherwise wait for).  Distributed default: 3 -- its all-to-alls run beside the
-  // first accumulations (h is accumulated last); 1 was -0.45 ms per rank against 0 at N = 8
-  // in the one-GPU rehearsal.
-  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 3 : 2);
+  // accumulation's launch; 4 = between the first sorts and the first accumulation.  Round 3,
+  // distributed H on its masked half of the CUs, at N = 8 in the one-GPU rehearsal: 1 (default)
+  // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
+  // thread 10.44 (not kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
+  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 1 : 2);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -1035,15 +1035,20 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (sorder[r] == big[0] || (nbig > 1 && h_pos != 1 && sorder[r] == big[1])) pre_sorts = r + 1;
   bool h_in_pre = false;
   for (int r = 0; r < pre_sorts; r++) h_in_pre = h_in_pre || jobs[sorder[r]].is_h;
-  if (h_in_pre && (h_mode == 2 || h_mode == 3)) h_mode = 1;  // h's own sort is among the first: H first
+  if (h_in_pre && (h_mode >= 2)) h_mode = 1;  // h's own sort is among the first: H first
   if (h_mode == 0 || h_mode == 1) {
     if ((s = enqueue_h(jev[33]))) return s;
   }
+
   for (int r = 0; r < pre_sorts; r++) {
     if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
     if ((s = sort_job(sorder[r], sS))) return s;
   }
   if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
+  // 4 = enqueued between the first sorts and the first accumulation: the sorts are not held up
+  // by the host's ~0.4 ms of H enqueueing (mode 1), and H's first kernels reach the device
+  // before the first accumulation fills every CU (mode 3)
+  if (h_mode == 4 && (s = enqueue_h(jev[33]))) return s;
   if (nbig > 0) {
     // wait for the last pre-sort that is a real sort: a trailing copy of another multiexp's
     // entries (b_g1_aux from b_g2_aux) is ~0.15 ms of blits that can run beside the accumulation
