@@ -310,8 +310,19 @@ static Jac<Fp> g1_from_xyzz(const XYZZ<G1F>& p) {
   return xyzz_to_jac(fp_from_dev_g1(p.X), fp_from_dev_g1(p.Y), fp_from_dev_g1(p.ZZ), fp_from_dev_g1(p.ZZZ));
 }
 // window sums -> the multiexp (Horner over the Wb windows, c doublings each; multiexp.rs:244-249),
-// or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction)
+// or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction), or
+// the same for each of two bucket halves
 Jac<Fp> combine_g1(const XYZZ<G1F>* ws, const MsmShape& sh) {
+  if (sh.halves) {  // two bucket halves (reduce_halves_shift)
+    auto dbl_n = [](Jac<Fp> z, int k) {
+      for (int i = 0; i < k; i++) z = jac_dbl(z);
+      return z;
+    };
+    Jac<Fp> lo = jac_add(g1_from_xyzz(ws[0]), dbl_n(g1_from_xyzz(ws[1]), reduce_halves_shift(sh, false, 0)));
+    Jac<Fp> hi = jac_add(g1_from_xyzz(ws[3]), dbl_n(g1_from_xyzz(ws[4]), reduce_halves_shift(sh, false, 1)));
+    hi = jac_add(hi, dbl_n(g1_from_xyzz(ws[5]), reduce_lg2((uint32_t)sh.NB / 2)));
+    return jac_add(lo, hi);
+  }
   const int shift = reduce_split_shift(sh, false);
   if (shift >= 0) {
     Jac<Fp> z = g1_from_xyzz(ws[1]);
@@ -332,6 +343,16 @@ static Jac<bh::Fp2> g2_from_xyzz(const XYZZ<Fp2Ops>& p) {
   return xyzz_to_jac(fp2_from_dev(p.X), fp2_from_dev(p.Y), fp2_from_dev(p.ZZ), fp2_from_dev(p.ZZZ));
 }
 Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh) {
+  if (sh.halves) {  // two bucket halves (reduce_halves_shift)
+    auto dbl_n = [](Jac<bh::Fp2> z, int k) {
+      for (int i = 0; i < k; i++) z = jac_dbl(z);
+      return z;
+    };
+    Jac<bh::Fp2> lo = jac_add(g2_from_xyzz(ws[0]), dbl_n(g2_from_xyzz(ws[1]), reduce_halves_shift(sh, true, 0)));
+    Jac<bh::Fp2> hi = jac_add(g2_from_xyzz(ws[3]), dbl_n(g2_from_xyzz(ws[4]), reduce_halves_shift(sh, true, 1)));
+    hi = jac_add(hi, dbl_n(g2_from_xyzz(ws[5]), reduce_lg2((uint32_t)sh.NB / 2)));
+    return jac_add(lo, hi);
+  }
   const int shift = reduce_split_shift(sh, true);
   if (shift >= 0) {
     Jac<bh::Fp2> z = g2_from_xyzz(ws[1]);

@@ -16,6 +16,11 @@ struct MsmShape {
   int Wb;   // bucket windows: W, or 1 with a window table (all windows share the buckets)
   int pre;  // 1: bases are a window table T[i*W + w] = 2^(c*w) * P_i (entry = i*W + w)
   int rec;  // u32 words per base record (0: packed affine, 2 x PACKED_WORDS)
+  // 1 (Wb == 1 only): the bucket set is accumulated and reduced as two halves, each with its own
+  // reduction chain, so the lower half's reduction runs beside the upper half's accumulation
+  // (the prover's last multiexp, msm_back); L2 = buckets per reduction thread of the upper half
+  int halves = 0;
+  int L2 = 0;
 };
 MsmShape msm_shape(size_t n, int c_override);
 // shape for a window table: c from the cost model n*ceil(256/c) + ~6.5 * 2^(c-1)
@@ -27,21 +32,35 @@ MsmShape msm_shape_table(size_t n, int c);
 // two points and the host finishes the window: out[0] + 2^reduce_split_shift() * out[1]
 // (the shift's doublings are a serial chain: cheaper on the host than on one device thread).
 uint32_t reduce_block_max(bool g2);  // BH_REDUCE_BT (A/B), default 256 (G1) / 128 (G2)
-inline uint32_t reduce_block_threads(const MsmShape& sh, bool g2) {
-  const uint32_t T = (uint32_t)(sh.NB / sh.L), bmax = reduce_block_max(g2);
+// (for a bucket range of nbr buckets, L per thread)
+inline uint32_t reduce_threads_for(uint32_t nbr, uint32_t L, bool g2) {
+  const uint32_t T = nbr / L, bmax = reduce_block_max(g2);
   return T < bmax ? T : bmax;
+}
+inline uint32_t reduce_block_threads(const MsmShape& sh, bool g2) {
+  return reduce_threads_for((uint32_t)sh.NB, (uint32_t)sh.L, g2);
 }
 inline int reduce_lg2(uint32_t x) {
   int r = 0;
   while ((1u << r) < x) r++;
   return r;
 }
+inline int reduce_shift_for(uint32_t nbr, uint32_t L, bool g2) {
+  return reduce_lg2(L) + reduce_lg2(reduce_threads_for(nbr, L, g2));
+}
 inline int reduce_split_shift(const MsmShape& sh, bool g2) {
-  return sh.Wb == 1 ? reduce_lg2((uint32_t)sh.L) + reduce_lg2(reduce_block_threads(sh, g2)) : -1;
+  return sh.Wb == 1 ? reduce_shift_for((uint32_t)sh.NB, (uint32_t)sh.L, g2) : -1;
+}
+// halves: out[0..3) is the lower half [0, NB/2): out[0] + 2^shift_lo * out[1]; out[3..6) the
+// upper half, reduced as a window of its own: out[3] + 2^shift_hi * out[4] + (NB/2) * out[5]
+// (out[5] = the plain sum of its buckets, each of which holds digit NB/2 more than its position)
+inline int reduce_halves_shift(const MsmShape& sh, bool g2, int upper) {
+  return reduce_shift_for((uint32_t)sh.NB / 2, (uint32_t)(upper ? sh.L2 : sh.L), g2);
 }
 
 struct MsmTiming {
   hipEvent_t ev_acc_begin = nullptr, ev_acc_end = nullptr;  // bracket k_accumulate_dev
+  hipEvent_t ev_half = nullptr;  // halves: recorded once the lower half is accumulated
 };
 
 template <class C>
@@ -87,9 +106,11 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 // max_span: the largest number of continuation partials of one bucket (max_span() below)
 // when known, so that only the continuation-tree levels that can do work are launched;
 // -1: every level a bucket could need
+// halves: the caller orders `st` after the lower half (MsmTiming::ev_half); msm_back enqueues
+// the lower half's reduction, waits for `acc_done` (the whole accumulation), then the upper's
 template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
-                    int max_span = -1);
+                    int max_span = -1, hipEvent_t acc_done = nullptr);
 
 size_t scan_scratch_words(size_t n);
 // max over buckets of (last segment - first segment) for segment length S: the

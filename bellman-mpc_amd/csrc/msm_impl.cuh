@@ -82,12 +82,13 @@ __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_
 template <class C, int F>
 __global__ void __launch_bounds__(256) k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
                                                     const uint32_t* offsets, uint32_t nbt, uint32_t S,
-                                                    uint32_t stride, typename C::P* conts) {
+                                                    uint32_t stride, uint32_t b_lo, uint32_t b_hi,
+                                                    typename C::P* conts) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t E = offsets[nbt];
   if ((size_t)s * S >= E) return;
   const uint32_t b = cont_bucket[s];
-  if (b == 0xffffffffu) return;
+  if (b == 0xffffffffu || b < b_lo || b >= b_hi) return;  // buckets [b_lo, b_hi) only
   const uint32_t off = offsets[b];
   const uint32_t s_first = off / S;
   const uint32_t ncont = (off + counts[b] - 1) / S - s_first;
@@ -117,14 +118,14 @@ inline size_t cont_seq_max() {
 // segments costs 4 + 2 serial additions instead of 15.  The tails are VALU-bound chains
 // on a small fraction of the SIMDs: serial depth is their latency.
 template <class C, int Q>
-__global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t nbt,
-                                                  uint32_t S, typename C::P* conts) {
+__global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
+                                                  uint32_t nbr, uint32_t S, typename C::P* conts) {
   extern __shared__ uint4 lds_raw[];
   typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t b = gid / Q, q = gid % Q;
+  const uint32_t b = b0 + gid / Q, q = gid % Q;  // buckets [b0, b0 + nbr)
   uint32_t s_first = 0, ncont = 0;
-  if (b < nbt) {
+  if (gid / Q < nbr) {
     const uint32_t cnt = counts[b];
     if (cnt) {
       const uint32_t off = offsets[b];
@@ -232,13 +233,13 @@ __device__ __forceinline__ void block_epilogue(typename C::P v, const typename C
 template <class C>
 __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
                                                        const typename C::P* bucket_sums, const typename C::P* conts,
-                                                       uint32_t S, uint32_t NB, uint32_t L, int lgL, uint32_t nblk,
-                                                       int fold, typename C::P* Y, typename C::P* Ssum) {
+                                                       uint32_t S, uint32_t b0, uint32_t NB, uint32_t L, int lgL,
+                                                       uint32_t nblk, int fold, typename C::P* Y, typename C::P* Ssum) {
   extern __shared__ uint4 lds_raw[];
   typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
   const uint32_t i = threadIdx.x;
   const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
-  const uint32_t gb0 = w * NB + (blk * blockDim.x + i) * L;
+  const uint32_t gb0 = b0 + w * NB + (blk * blockDim.x + i) * L;
   // G2 (448-byte points, one wave per SIMD): the running total `acc` waits in this thread's LDS
   // slot (free until the epilogue) instead of registers, which the compiler otherwise spills
   // to scratch (KB per lane)
@@ -296,7 +297,8 @@ __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, c
 // thread j owns blocks [j*Lb, j*Lb + Lb): P_j = sum Y, A'_j = sum_k k S, R'_j = sum_k S, and
 //   sum_blk blk S = sum_j (A'_j + Lb * V'_j),  V'_j = sum_{j' > j} R'_j'
 // -> out[w] = the window total (canonical coordinates); split (one window): out[0] = sum P,
-// out[1] = sum_blk blk * S, and the host adds 2^lgM * out[1] (reduce_split_shift).
+// out[1] = sum_blk blk * S, out[2] = sum_blk S, and the host adds 2^lgM * out[1]
+// (reduce_split_shift; out[2] is the plain bucket sum a bucket range's offset multiplies).
 template <class C>
 __global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
                                                        uint32_t nblk, uint32_t Lb, int lgLb, int lgM, int split,
@@ -318,12 +320,13 @@ __global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, c
     else if (op == 1) run = r;
     else p = r;
   }
-  typename C::P s_unused;
-  block_epilogue<C>(run, acc, lgLb, p, split ? -1 : lgM, split != 0, lds, &s_unused);
+  typename C::P s_all;
+  block_epilogue<C>(run, acc, lgLb, p, split ? -1 : lgM, split != 0, lds, &s_all);
   if (i == 0) {
     if (split) {
       out[0] = C::reduce(load_point<C>(&lds[blockDim.x]));
       out[1] = C::reduce(load_point<C>(&lds[0]));
+      out[2] = C::reduce(s_all);
     } else {
       out[w] = C::reduce(load_point<C>(&lds[0]));
     }
@@ -336,21 +339,24 @@ __global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, c
 // segment.  The next entry's affine base is prefetched global -> LDS by
 // global_load_lds_dwordx4 (no VGPR cost) while the current mixed addition runs: each wave
 // owns NQ x 64 x 16 B of LDS, lane l's base occupying slot l of each of the NQ rows.
+// Only the entries of buckets [b_lo, b_hi) (MsmShape::halves: two launches); a segment cut by
+// the range keeps the continuation bookkeeping of the whole segment.
 // (A register-load variant without the prefetch measured slower and was removed.)
 template <class C>
 __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
-                                                       typename C::P* bucket_sums, typename C::P* conts,
-                                                       uint32_t* cont_bucket) {
+                                                       uint32_t b_lo, uint32_t b_hi, typename C::P* bucket_sums,
+                                                       typename C::P* conts, uint32_t* cont_bucket) {
   using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
   constexpr int PW = F::PACKED_WORDS;
   constexpr int NQ = 2 * PW / 4;  // 16-byte pieces per affine base
   __shared__ uint4 pre[4][NQ][64];
-  const uint32_t E = offsets[nbt];
+  const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t pos0 = seg * S;
-  if (pos0 >= E) return;
-  const uint32_t end = min(pos0 + S, E);
+  const uint32_t start = max(pos0, E_lo);
+  if (pos0 >= E_hi || start >= pos0 + S) return;
+  const uint32_t end = min(pos0 + S, E_hi);
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   auto issue = [&](uint32_t e) {
     const uint32_t* src = bases + (size_t)(e & 0x7fffffffu) * rec;
@@ -359,15 +365,15 @@ __global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, 
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
                                        (__attribute__((address_space(3))) void*)&pre[wv][q][0], 16, 0, 0);
   };
-  uint32_t e_cur = entries[pos0];
+  uint32_t e_cur = entries[start];
   issue(e_cur);
-  uint32_t e_next = (pos0 + 1 < end) ? entries[pos0 + 1] : 0u;
-  uint32_t b = find_bucket(offsets, nbt, pos0);
+  uint32_t e_next = (start + 1 < end) ? entries[start + 1] : 0u;
+  uint32_t b = find_bucket(offsets, nbt, start);
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
-  cont_bucket[seg] = started_here ? 0xffffffffu : b;
+  if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
   typename C::P acc = C::identity();
-  for (uint32_t j = pos0; j < end; j++) {
+  for (uint32_t j = start; j < end; j++) {
     if (j == next) {
       if (started_here) store_point<C>(&bucket_sums[b], acc);
       else store_point<C>(&conts[seg], acc);
@@ -582,9 +588,16 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
+    const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
     hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                       ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, ws.bucket_sums, ws.conts,
+                       ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, 0u, cut, ws.bucket_sums, ws.conts,
                        ws.cont_bucket);
+    if (sh.halves) {
+      if (timing && timing->ev_half) hipEventRecord(timing->ev_half, st);
+      hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, cut, (uint32_t)nbt, ws.bucket_sums,
+                         ws.conts, ws.cont_bucket);
+    }
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
   }
   return hipGetLastError();
@@ -599,11 +612,48 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
   return msm_accumulate<C>(ws, st, d_bases, n, sh, timing);
 }
 
-// Back half: continuation fix-up, summation by parts and the per-window sums, copied to host_out (W entries).
+// Reduction of the buckets [b0, b0 + nbr) of each of Wb windows (window stride NB): continuation
+// fix-up, then the two-level summation by parts into out[] (Wb totals, or 3 points when split).
+template <class C>
+static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, size_t segs, size_t span,
+                         bool fold, bool seq, uint32_t b0, uint32_t nbr, uint32_t L, uint32_t y_off,
+                         typename C::P* out) {
+  constexpr bool G2 = sizeof(typename C::P) > 256;
+  const size_t nb_all = (size_t)sh.Wb * nbr;
+  if (!fold && seq) {
+    constexpr int Q = 4;
+    constexpr uint32_t B = G2 ? 128 : 256;  // LDS: B points
+    if (span >= 2)
+      hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nb_all * Q, B)), dim3(B), B * sizeof(typename C::P),
+                         st, ws.counts, ws.offsets, b0, (uint32_t)nb_all, (uint32_t)sh.S, ws.conts);
+  } else if (!fold) {
+    const size_t nbt = (size_t)sh.Wb * sh.NB;
+    for (size_t stride = 1; stride < span; stride *= 4)
+      hipLaunchKernelGGL((k_cont_treeF<C, 4>), dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
+                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, (uint32_t)stride, b0,
+                         (uint32_t)(b0 + nb_all), ws.conts);
+  }
+  // two-level summation by parts (k_reduce_blocks, k_reduce_window): Y/S per level-1 block
+  // in seg_weighted / seg_sum (from y_off), the totals in out
+  const uint32_t T = nbr / L;
+  const uint32_t BT = reduce_threads_for(nbr, L, G2);
+  const uint32_t nblk = T / BT;
+  const uint32_t BT2 = std::min(nblk, G2 ? 128u : 256u);
+  const uint32_t Lb = nblk / BT2;
+  const int split = sh.Wb == 1 ? 1 : 0;
+  hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
+                     ws.counts, ws.offsets, ws.bucket_sums, ws.conts, (uint32_t)sh.S, b0, (uint32_t)sh.NB, L,
+                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted + y_off, ws.seg_sum + y_off);
+  hipLaunchKernelGGL(k_reduce_window<C>, dim3((unsigned)sh.Wb), dim3(BT2), 2 * BT2 * sizeof(typename C::P), st,
+                     ws.seg_weighted + y_off, ws.seg_sum + y_off, nblk, Lb, reduce_lg2(Lb),
+                     reduce_lg2(L) + reduce_lg2(BT), split, out);
+}
+
+// Back half: continuation fix-up, summation by parts and the per-window sums, copied to host_out
+// (Wb entries; 2 for one shared window; 6 for halves, see reduce_halves_shift).
 template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
-                    int max_span) {
-  const size_t nbt = (size_t)sh.Wb * sh.NB;
+                    int max_span, hipEvent_t acc_done) {
   // continuation partials: a bucket spanning up to REDUCE_FOLD_SPAN segments has them added
   // by its reduction thread (no extra launch); longer spans (known from the sort) are folded
   // first -- Q threads per bucket, or log-depth 4-ary tree levels
@@ -614,34 +664,19 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
   const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;
-  if (!fold && max_span >= 0 && span <= cont_seq_max()) {
-    constexpr int Q = 4;
-    constexpr uint32_t B = sizeof(typename C::P) > 256 ? 128 : 256;  // LDS: B points
-    if (span >= 2)
-      hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nbt * Q, B)), dim3(B), B * sizeof(typename C::P), st,
-                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, ws.conts);
-  } else if (!fold) {
-    for (size_t stride = 1; stride < span; stride *= 4)
-      hipLaunchKernelGGL((k_cont_treeF<C, 4>), dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
-                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, (uint32_t)stride, ws.conts);
+  const bool seq = max_span >= 0 && span <= cont_seq_max();
+  if (sh.halves) {
+    const uint32_t nbh = (uint32_t)sh.NB / 2;
+    reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums);
+    if (acc_done) hipStreamWaitEvent(st, acc_done, 0);
+    const uint32_t y_off = nbh / sh.L / reduce_threads_for(nbh, (uint32_t)sh.L, sizeof(typename C::P) > 256);
+    reduce_range<C>(ws, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3);
+    hipMemcpyAsync(host_out, ws.window_sums, 6 * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+    return hipGetLastError();
   }
-  // two-level summation by parts (k_reduce_blocks, k_reduce_window): Y/S per level-1 block
-  // in seg_weighted / seg_sum, the window totals in window_sums
-  constexpr bool G2 = sizeof(typename C::P) > 256;
-  const uint32_t L = (uint32_t)sh.L;
-  const uint32_t T = (uint32_t)(sh.NB / L);
-  const uint32_t BT = reduce_block_threads(sh, G2);
-  const uint32_t nblk = T / BT;
-  const uint32_t BT2 = std::min(nblk, G2 ? 128u : 256u);
-  const uint32_t Lb = nblk / BT2;
-  const int split = reduce_split_shift(sh, G2) >= 0 ? 1 : 0;
-  hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
-                     ws.counts, ws.offsets, ws.bucket_sums, ws.conts, (uint32_t)sh.S, (uint32_t)sh.NB, L,
-                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted, ws.seg_sum);
-  hipLaunchKernelGGL(k_reduce_window<C>, dim3((unsigned)sh.Wb), dim3(BT2), 2 * BT2 * sizeof(typename C::P), st,
-                     ws.seg_weighted, ws.seg_sum, nblk, Lb, reduce_lg2(Lb), reduce_lg2(L) + reduce_lg2(BT), split,
-                     ws.window_sums);
-  hipMemcpyAsync(host_out, ws.window_sums, (split ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
+  reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums);
+  hipMemcpyAsync(host_out, ws.window_sums, (sh.Wb == 1 ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost,
+                 st);
   return hipGetLastError();
 }
 

@@ -924,6 +924,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     MsmTiming tm;
     tm.ev_acc_begin = acc_events_on() ? jev[2 * j] : nullptr;
     tm.ev_acc_end = acc_events_on() ? jev[2 * j + 1] : nullptr;
+    tm.ev_half = shapes[j].halves ? jev[36 + j] : nullptr;
     const uint32_t* bases = use_table[j] ? J.srs->win_global() : J.srs->pts.as<uint32_t>();
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
@@ -940,7 +941,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   auto tail_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
-    BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + j], 0));
+    // halves: from the lower half's end; msm_back waits for the rest before the upper half
+    BH_TRY_HIP(hipStreamWaitEvent(st, jev[(shapes[j].halves ? 36 : 24) + j], 0));
     if (tail_defer && last_acc >= 0) BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + last_acc], 0));
     // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
     // (copied here, off the accumulation stream)
@@ -952,8 +954,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
       span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS, (size_t)shapes[j].Wb * shapes[j].NB);
     }
-    if (J.g2) BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span));
-    else BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span));
+    if (J.g2)
+      BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span, jev[24 + j]));
+    else
+      BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span, jev[24 + j]));
     return BH_OK;
   };
   BH_TRY_HIP(hipEventRecord(jev[33], sS));
@@ -981,10 +985,30 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       const char* e = getenv("BH_LAST_TAIL_THREADS");
       return e ? atoi(e) : 65536;
     }();
+    // BH_LAST_HALVES=1: with one shared bucket window, the last multiexp is accumulated as two
+    // bucket halves and the lower half's reduction (work-lean L) runs beside the upper half's
+    // accumulation: only the upper half's, with the short chains, is left at the end.  Parity
+    // green, but +0.8 ms per 2^22 proof (60.79 against 60.00 ms, profiles/r03_ab_last_halves.txt):
+    // the lower half's latency-bound reduction slows the upper accumulation by more than the
+    // shorter tail saves.  Off by default.
+    static const bool last_halves = [] {
+      const char* e = getenv("BH_LAST_HALVES");
+      return e && e[0] == '1';
+    }();
+    const bool halves = last_halves && sl.Wb == 1 && sl.NB >= 4096 && !serial;
     if (last_threads > 0) {
+      const int nb = halves ? sl.NB / 2 : sl.NB;
       int L = sl.L;
-      while (L > 1 && (size_t)sl.Wb * (size_t)(sl.NB / L) < (size_t)last_threads) L >>= 1;
-      sl.L = L;
+      while (L > 1 && (size_t)sl.Wb * (size_t)(nb / L) < (size_t)last_threads) L >>= 1;
+      if (halves) {
+        sl.halves = 1;
+        sl.L2 = L;
+      } else {
+        sl.L = L;
+      }
+    } else if (halves) {
+      sl.halves = 1;
+      sl.L2 = sl.L;
     }
     // BH_LAST_ACC_ROUNDS = r (A/B experiments): the last accumulation in r resident rounds instead
     // of fit_segments' 4 (longer segments: fewer continuation partials for its tail to fold)
