@@ -131,6 +131,13 @@ def _load():
         "bh_chain_assignment": (I, [S, U64, U64, P, P, P, P, P, P, P, P]),
         "bh_comm_allreduce_max": (I, [P, P]),
         "bh_comm_info": (I, [P, P]),
+        "bh_params_vector": (I, [P, I, P]),
+        "bh_scalars_upload": (I, [P, P, S, I, P]),
+        "bh_compute_h_scalars": (I, [P, P, P, P, S, P]),
+        "bh_scalars_len": (S, [P]),
+        "bh_scalars_free": (I, [P]),
+        "bh_multiexp_submit_scalars": (I, [P, P, S, P, S, P, P]),
+        "bh_scalars_sync": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -155,7 +162,10 @@ EXPORTED_SYMBOLS = [
     "bh_comm_allgather", "bh_comm_allreduce_max", "bh_comm_info", "bh_params_prepare_shard", "bh_last_stats",
     "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
     "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch", "bh_verify_proof", "bh_verify_batch",
+    "bh_params_vector", "bh_scalars_upload", "bh_compute_h_scalars", "bh_scalars_len", "bh_scalars_free",
+    "bh_multiexp_submit_scalars", "bh_scalars_sync",
 ]
+BH_VEC_H, BH_VEC_L, BH_VEC_A, BH_VEC_B_G1, BH_VEC_B_G2 = range(5)
 PARTIAL_BYTES = 960
 
 
@@ -202,6 +212,30 @@ def fr_to_canonical_limbs(values):
         x = int(v) % R_MODULUS
         out[i] = [(x >> (64 * k)) & 0xFFFFFFFFFFFFFFFF for k in range(4)]
     return out
+
+
+class DensityWords:
+    """A DensityTracker already in bitvec Lsb0 words (n bits), e.g. chain_assignment's maps."""
+
+    def __init__(self, words, n):
+        self.words, self.n = np.ascontiguousarray(words, dtype=np.uint64), int(n)
+
+    def total(self):
+        full, rem = self.n // 64, self.n % 64
+        t = sum(bin(int(x)).count("1") for x in self.words[:full])
+        if rem:
+            t += bin(int(self.words[full]) & ((1 << rem) - 1)).count("1")
+        return t
+
+
+def _density(density):
+    """-> (words or None, nbits)"""
+    if density is None or isinstance(density, FullDensity) or density is FullDensity:
+        return None, 0
+    if isinstance(density, DensityWords):
+        return density.words, density.n
+    bits = density.bv if hasattr(density, "bv") else list(density)
+    return density_words(bits), len(bits)
 
 
 def density_words(bits):
@@ -301,12 +335,9 @@ def multiexp(ctx, bases, offset, density, exponents, montgomery=False):
     else:
         ex = fr_to_mont(exponents) if montgomery else fr_to_canonical_limbs(exponents)
     n = ex.shape[0]
-    bits = None
-    if density is not None and not isinstance(density, FullDensity) and density is not FullDensity:
-        bits = density.bv if hasattr(density, "bv") else list(density)
-    dw = density_words(bits) if bits is not None else None
+    dw, nbits = _density(density)
     out = np.zeros(96 if bases.group == BH_G1 else 192, dtype=np.uint8)
-    _check(_lib.bh_multiexp(ctx.h, bases.h, offset, _ptr(dw), len(bits) if bits is not None else 0,
+    _check(_lib.bh_multiexp(ctx.h, bases.h, offset, _ptr(dw), nbits,
                             _ptr(ex) if n else None, n,
                             BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, _ptr(out)),
            "bh_multiexp")
@@ -342,19 +373,91 @@ class Waiter:
                 pass
 
 
+class Scalars:
+    """A device-resident Arc<Vec<Fr::Repr>> (bh_scalars): uploaded once (bh_scalars_upload) or
+    produced on the device (compute_h_scalars), read by any number of multiexp_async calls."""
+
+    def __init__(self, ctx, exponents=None, montgomery=False, _handle=None):
+        self.ctx = ctx
+        if _handle is not None:
+            self.h = _handle
+            return
+        if isinstance(exponents, np.ndarray):
+            ex = np.ascontiguousarray(exponents, dtype=np.uint64).reshape(-1, 4)
+        else:
+            ex = fr_to_mont(exponents) if montgomery else fr_to_canonical_limbs(exponents)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_scalars_upload(ctx.h, _ptr(ex) if ex.shape[0] else None, ex.shape[0],
+                                      BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL,
+                                      ctypes.byref(h)), "bh_scalars_upload")
+        self.h = h
+
+    def __len__(self):
+        return _lib.bh_scalars_len(self.h)
+
+    def sync(self):
+        """bh_scalars_sync: the producer has read its host buffers (and reports the H status)."""
+        _check(_lib.bh_scalars_sync(self.h), "bh_scalars_sync")
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.bh_scalars_free(self.h)  # returns once a producer no longer reads _keep
+            self.h = None
+        self._keep = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def compute_h_scalars(ctx, a, b, c):
+    """The H block (prover.rs:210-231) leaving h on the device: a Scalars of m-1 entries.
+    a, b, c: (n,4) Montgomery arrays (or lists of ints); computed asynchronously."""
+    A, B, C = (np.ascontiguousarray(x, dtype=np.uint64).reshape(-1, 4) if isinstance(x, np.ndarray)
+               else fr_to_mont(x) for x in (a, b, c))
+    n = A.shape[0]
+    assert B.shape[0] == n and C.shape[0] == n
+    h = ctypes.c_void_p()
+    _check(_lib.bh_compute_h_scalars(ctx.h, _ptr(A), _ptr(B), _ptr(C), n, ctypes.byref(h)), "bh_compute_h_scalars")
+    out = Scalars(ctx, _handle=h)
+    out._keep = (A, B, C)  # read asynchronously: referenced until sync() or close()
+    return out
+
+
+class ParamsBases:
+    """A Parameters vector as multiexp bases (ParameterSource::get_*, groth16/mod.rs:414-477):
+    borrowed from the Parameters, which it keeps referenced."""
+
+    def __init__(self, params, which):
+        h = ctypes.c_void_p()
+        _check(_lib.bh_params_vector(params.h, which, ctypes.byref(h)), "bh_params_vector")
+        self.h, self.params = h, params
+        self.group = BH_G2 if which == BH_VEC_B_G2 else BH_G1
+
+    def __len__(self):
+        return _lib.bh_srs_len(self.h)
+
+
 def multiexp_async(ctx, bases, offset, density, exponents, montgomery=False):
-    """multiexp::multiexp returning a Waiter (bh_multiexp_submit); arguments as multiexp()."""
+    """multiexp::multiexp returning a Waiter (bh_multiexp_submit); arguments as multiexp(), or
+    exponents = a Scalars (device-resident; bh_multiexp_submit_scalars)."""
+    if isinstance(exponents, Scalars):
+        dw, nbits = _density(density)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_multiexp_submit_scalars(ctx.h, bases.h, offset, _ptr(dw), nbits, exponents.h,
+                                               ctypes.byref(h)), "bh_multiexp_submit_scalars")
+        return Waiter(h, bases.group, ctx, (bases, exponents))
     if isinstance(exponents, np.ndarray):
         ex = np.ascontiguousarray(exponents, dtype=np.uint64).reshape(-1, 4)
     else:
         ex = fr_to_mont(exponents) if montgomery else fr_to_canonical_limbs(exponents)
     n = ex.shape[0]
-    bits = None
-    if density is not None and not isinstance(density, FullDensity) and density is not FullDensity:
-        bits = density.bv if hasattr(density, "bv") else list(density)
-    dw = density_words(bits) if bits is not None else None
+    dw, nbits = _density(density)
     h = ctypes.c_void_p()
-    _check(_lib.bh_multiexp_submit(ctx.h, bases.h, offset, _ptr(dw), len(bits) if bits is not None else 0,
+    _check(_lib.bh_multiexp_submit(ctx.h, bases.h, offset, _ptr(dw), nbits,
                                    _ptr(ex) if n else None, n,
                                    BH_SCALARS_MONTGOMERY if montgomery else BH_SCALARS_CANONICAL, ctypes.byref(h)),
            "bh_multiexp_submit")
@@ -457,6 +560,10 @@ class Parameters:
         out = np.zeros(n.value, dtype=np.uint8)
         _check(_lib.bh_params_write(self.h, _ptr(out), n.value, ctypes.byref(n)))
         return out.tobytes()
+
+    def vector(self, which):
+        """ParameterSource::get_h/get_l/get_a/get_b_g1/get_b_g2: BH_VEC_* -> multiexp bases."""
+        return ParamsBases(self, which)
 
     def prepare(self, witness, nshards=1):
         """Build the prover window tables now rather than inside the first proof."""
@@ -672,6 +779,30 @@ def prove(ctx, params, asg, r, s):
                          A[3].shape[0], _ptr(A[4]), A[4].shape[0], _ptr(D[0]), _ptr(D[1]), _ptr(D[2]), _ptr(rr),
                          _ptr(ss), _ptr(out)), "bh_prove")
     return out.tobytes()
+
+
+def prove_seam(ctx, params, asg, r, s):
+    """create_proof after synthesis (prover.rs:206-349) through the multiexp seam alone, as a
+    Rust caller that swaps only multiexp() and the H block sees it: h on the device
+    (bh_compute_h_scalars), the assignments uploaded once (the Arcs of prover.rs:233-250), the
+    eight multiexps in flight on the Parameters' own vectors (get_h ... get_b_g2, so their window
+    tables apply), waited, and the proof assembled on the host (prover.rs:315-349).
+    asg: dict as returned by chain_assignment.  Byte-equal to prove()."""
+    ni, na = asg["inputs"].shape[0], asg["aux"].shape[0]
+    h = compute_h_scalars(ctx, asg["a"], asg["b"], asg["c"])
+    inp = Scalars(ctx, asg["inputs"], montgomery=True)
+    aux = Scalars(ctx, asg["aux"], montgomery=True)
+    a_aux = DensityWords(asg["a_aux_density"], na)
+    b_in = DensityWords(asg["b_input_density"], ni)
+    b_aux = DensityWords(asg["b_aux_density"], na)
+    b_in_total = b_in.total()
+    H, L, A, B1, B2 = (params.vector(k) for k in (BH_VEC_H, BH_VEC_L, BH_VEC_A, BH_VEC_B_G1, BH_VEC_B_G2))
+    waiters = [multiexp_async(ctx, H, 0, None, h), multiexp_async(ctx, L, 0, None, aux),
+               multiexp_async(ctx, A, 0, None, inp), multiexp_async(ctx, A, ni, a_aux, aux),
+               multiexp_async(ctx, B1, 0, b_in, inp), multiexp_async(ctx, B1, b_in_total, b_aux, aux),
+               multiexp_async(ctx, B2, 0, b_in, inp), multiexp_async(ctx, B2, b_in_total, b_aux, aux)]
+    partial = b"".join(w.wait() for w in waiters)
+    return proof_from_partials(params.vk_bytes(), partial, 1, r, s)
 
 
 def prove_batch(ctx, params, witnesses, r, s, lanes=0):

@@ -490,7 +490,7 @@ static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const F
 }
 
 void ctx_sync_all(bh_ctx* ctx) {
-  for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d})
+  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d, ctx->bg.st})
     if (st) (void)hipStreamSynchronize(st);
   for (hipStream_t st : ctx->tstream)
     if (st) (void)hipStreamSynchronize(st);
@@ -807,8 +807,16 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   for (bh_ctx* v : ctx->lanes) bh_ctx_destroy(v);
   ctx->lanes.clear();
   (void)hipSetDevice(ctx->device);
-  ctx_sync_all(ctx);  // nothing may still read the workspaces released below
+  {  // bh_compute_h_scalars producers still uploading: their deferred multiexps enqueue first
+    std::unique_lock<std::mutex> lk(ctx->bg.count_mu);
+    ctx->bg.cv.wait(lk, [&] { return ctx->bg.active == 0; });
+  }
+  ctx_sync_all(ctx);  // nothing may still read the workspaces released below (jobs' too)
   bh_ctx_release_jobs(ctx);
+  if (ctx->bg.st) (void)hipStreamDestroy(ctx->bg.st);
+  ctx->bg.ring.release();
+  ctx->bg.pool.reset();
+  ctx->bg.abc.release();
   if (ctx->h2d) (void)hipStreamSynchronize(ctx->h2d);
   ctx->ring.release();
   ctx->pool.reset();
@@ -1034,6 +1042,151 @@ bh_status bh_mul_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len)
 }
 bh_status bh_sub_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len) {
   return host_pointwise(ctx, a, b, len, 1);
+}
+
+// ---- the multiexp seam on device-resident data (include/bellman_hip.h)
+bh_status bh_params_vector(const bh_params* p, int which, const bh_srs** out) {
+  if (!p || !out) return BH_ERR_INVALID_ARGUMENT;
+  switch (which) {
+    case BH_VEC_H: *out = &p->h; return BH_OK;
+    case BH_VEC_L: *out = &p->l; return BH_OK;
+    case BH_VEC_A: *out = &p->a; return BH_OK;
+    case BH_VEC_B_G1: *out = &p->b_g1; return BH_OK;
+    case BH_VEC_B_G2: *out = &p->b_g2; return BH_OK;
+    default: return BH_ERR_INVALID_ARGUMENT;
+  }
+}
+
+static bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out) {
+  static std::atomic<uint64_t> next_id{1};
+  auto buf = std::make_shared<bh_scalar_buf>();
+  buf->device = ctx->device;
+  buf->id = next_id.fetch_add(1);
+  BH_TRY_HIP(buf->d.alloc(std::max<size_t>(n, 1) * 32));
+  BH_TRY_HIP(hipEventCreateWithFlags(&buf->ready, hipEventDisableTiming));
+  *out = std::move(buf);
+  return BH_OK;
+}
+
+bh_status bh_scalars_upload(bh_ctx* ctx, const uint64_t* exponents, size_t n, int scalar_format, bh_scalars** out) {
+  if (!ctx || !out || (n && !exponents)) return BH_ERR_INVALID_ARGUMENT;
+  if (scalar_format != BH_SCALARS_CANONICAL && scalar_format != BH_SCALARS_MONTGOMERY) return BH_ERR_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
+  std::shared_ptr<bh_scalar_buf> buf;
+  bh_status s = new_scalar_buf(ctx, n, &buf);
+  if (s) return s;
+  // on the copy stream (never behind compute); bh_compute_h_scalars' producer pauses its own
+  // upload meanwhile, so these vectors (read by the first sorts) land first
+  if (n) {
+    ctx->bg.fg_uploads++;
+    hipError_t e = ctx->ring.copy(ctx_pool(ctx), buf->d.p, exponents, n * 32, ctx->h2d);
+    ctx->bg.fg_uploads--;
+    BH_TRY_HIP(e);
+    BH_TRY_HIP(scalars_prepare(buf->d.as<uint32_t>(), buf->d.as<uint32_t>(), n,
+                               scalar_format == BH_SCALARS_MONTGOMERY ? 1 : 0, 0, ctx->h2d));
+  }
+  BH_TRY_HIP(hipEventRecord(buf->ready, ctx->h2d));
+  *out = new bh_scalars{n, std::move(buf)};
+  return BH_OK;
+}
+
+size_t bh_scalars_len(const bh_scalars* s) { return s ? s->n : 0; }
+
+bh_status bh_scalars_free(bh_scalars* s) {
+  if (s && s->buf) s->buf->wait_enqueued();  // a producer has read the caller's host buffers
+  delete s;  // the device vector lives on while a submitted multiexp still reads it
+  return BH_OK;
+}
+
+bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c, size_t nc,
+                               bh_scalars** h_out) {
+  if (!ctx || (nc && (!a || !b || !c)) || !h_out) return BH_ERR_INVALID_ARGUMENT;
+  size_t m;
+  uint32_t L;
+  bh_status s = bh_domain_size(nc, &m, &L);
+  if (s) return s;
+  Domain* D;
+  std::shared_ptr<bh_scalar_buf> buf;
+  {
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    BH_TRY_HIP(hipSetDevice(ctx->device));
+    if ((s = ctx_domain(ctx, (int)L, &D))) return s;  // built here: the domain map is ctx->mu's
+    if ((s = new_scalar_buf(ctx, m - 1, &buf))) return s;
+  }
+  buf->enqueued = false;
+  {
+    std::lock_guard<std::mutex> lk(ctx->bg.count_mu);
+    ctx->bg.active++;
+  }
+  // The producer holds no reference to the vector (its destructor joins the producer); the
+  // caller's a, b, c stay borrowed until the upload has read them (bh_scalars_sync)
+  bh_scalar_buf* raw = buf.get();
+  raw->producer = std::thread([ctx, raw, a, b, c, nc, m, D] {
+    auto run = [&]() -> bh_status {
+      auto& bg = ctx->bg;
+      std::lock_guard<std::mutex> lk(bg.mu);
+      BH_TRY_HIP(hipSetDevice(ctx->device));
+      if (!bg.st) {
+        // high priority, like the prover's H stream: its passes must not starve beside the
+        // accumulations (the multiexp on h sorts only after them)
+        int lo = 0, hi = 0;
+        BH_TRY_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        BH_TRY_HIP(hipStreamCreateWithPriority(&bg.st, hipStreamNonBlocking, hi));
+        BH_TRY_HIP(bg.ring.init());
+        bg.pool.reset(new HostPool(3));
+      }
+      BH_TRY_HIP(bg.abc.alloc(3 * m * 32));  // stream order on bg.st protects it across producers
+      uint32_t* abc = bg.abc.as<uint32_t>();
+      const uint64_t* src[3] = {a, b, c};
+      for (int v = 0; v < 3; v++) {
+        uint32_t* dst = abc + (size_t)v * m * 8;
+        if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.st));
+        if (nc) {
+          // in 32 MB pieces, paused while a bh_scalars_upload streams (the assignments feed the
+          // first sorts; H is needed last)
+          const size_t piece = (size_t)32 << 20;
+          for (size_t off = 0; off < nc * 32; off += piece) {
+            while (bg.fg_uploads.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            BH_TRY_HIP(bg.ring.copy(*bg.pool, reinterpret_cast<uint8_t*>(dst) + off,
+                                    reinterpret_cast<const uint8_t*>(src[v]) + off, std::min(piece, nc * 32 - off),
+                                    bg.st));
+          }
+          launch_fr_convert(dst, dst, nc, fr_to_dev_const(), 0, bg.st);
+        }
+      }
+      // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
+      bh_status hs = run_h_pipeline(ctx, D, abc, bg.st, nullptr, raw->d.as<uint32_t>());
+      if (hs) return hs;
+      BH_TRY_HIP(hipEventRecord(raw->ready, bg.st));
+      return BH_OK;
+    };
+    const bh_status st = run();
+    if (st) {  // nothing waits for `ready`: make it a completed event
+      (void)hipEventRecord(raw->ready, nullptr);
+    }
+    {
+      std::lock_guard<std::mutex> lk(raw->mu);
+      raw->status = st;
+      for (auto& f : raw->deferred) f(st);
+      raw->deferred.clear();
+      raw->enqueued = true;
+    }
+    raw->cv.notify_all();
+    {
+      std::lock_guard<std::mutex> lk(ctx->bg.count_mu);
+      ctx->bg.active--;
+    }
+    ctx->bg.cv.notify_all();
+  });
+  *h_out = new bh_scalars{m - 1, std::move(buf)};
+  return BH_OK;
+}
+
+bh_status bh_scalars_sync(bh_scalars* s) {
+  if (!s || !s->buf) return BH_ERR_INVALID_ARGUMENT;
+  s->buf->wait_enqueued();
+  return s->buf->status;
 }
 
 bh_status bh_compute_h(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c, size_t nc,

@@ -2,10 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -78,6 +83,19 @@ struct bh_job_registry {
   bool alive = true;                       // false once the context is destroyed
   std::vector<bh_job_slot*> all_slots, free_slots;
   std::vector<bh_job*> pending;            // submitted, not yet waited for
+  // recent digit sorts, by what determines them (jobs.hip: a job with the same scalars, density
+  // map, base offset and digit geometry copies the sorted entries instead of sorting again, as
+  // bh_prove does for b_g1_aux / b_g2_aux); valid while the slot has not been taken again
+  struct SortRec {
+    uint64_t scalars_id = 0;  // bh_scalar_buf::id (never reused)
+    uint64_t dens_hash = 0;
+    size_t n = 0, base_offset = 0;
+    int c = 0, W = 0, NB = 0, Wb = 0, pre = 0;
+    bh_job_slot* slot = nullptr;
+    int group = 0;
+    uint64_t use = 0;
+  };
+  std::vector<SortRec> sorts;
 };
 
 struct bh_srs {
@@ -89,13 +107,17 @@ struct bh_srs {
   // prover window table (built lazily, see prepare_tables in prover.hip) over the bases
   // [win_lo, win_hi) -- a shard's slice or the whole vector:
   // win[(i - win_lo)*win_W + w] = 2^(win_c*w) * P_i, packed affine, one record per win_rec words
-  bh::DevBuf win;
+  // (shared: an asynchronous multiexp reading the table holds it until its wait, so a rebuild
+  // never frees or overwrites a table under a job in flight; win_mu guards the fields for those
+  // readers, the prover reads them under its Parameters lock)
+  std::shared_ptr<bh::DevBuf> win = std::make_shared<bh::DevBuf>();
+  mutable std::mutex win_mu;
   int win_c = 0, win_W = 0, win_rec = 0;  // win_rec: u32 words per record (128-B aligned)
   size_t win_lo = 0, win_hi = 0;
   // the table addressed by GLOBAL base index (entries encode i*W + w): the allocation shifted
   // back by win_lo records (only indices in [win_lo, win_hi) are ever formed)
   const uint32_t* win_global() const {
-    return reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(win.p) -
+    return reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(win->p) -
                                              (uintptr_t)win_lo * (uintptr_t)win_W * (uintptr_t)win_rec * 4u);
   }
   bool win_covers(int c, size_t lo, size_t hi) const { return win_c == c && win_c && win_lo <= lo && hi <= win_hi; }
@@ -122,6 +144,44 @@ struct bh_params {
   std::mutex head_mu;
   std::vector<bh::AffinePt<bh::Fp>> h_a_head, h_b1_head;
   std::vector<bh::AffinePt<bh::Fp2>> h_b2_head;
+};
+
+constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use plain windows
+
+// A device-resident scalar vector (bh_scalars_upload, bh_compute_h_scalars): canonical packed
+// Fr (8 LE u32 each), shared by every multiexp submitted on it; `ready` is recorded once the
+// producing stream has written it (submits order their streams after it).
+// bh_compute_h_scalars produces it from a host thread (`producer`: the a, b, c upload and the H
+// passes): until that thread has enqueued its work (`enqueued`), `ready` is not recorded yet, so
+// multiexps submitted meanwhile park their own enqueue in `deferred`, which the producer runs,
+// under mu, right after recording `ready` (argument: the producer's status).
+struct bh_scalar_buf {
+  bh::DevBuf d;
+  uint64_t id = 0;  // unique per vector (jobs' sort sharing is keyed on it, not on d's address)
+  hipEvent_t ready = nullptr;
+  int device = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool enqueued = true;
+  bh_status status = BH_OK;
+  std::vector<std::function<void(bh_status)>> deferred;
+  std::thread producer;
+  void wait_enqueued() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return enqueued; });
+  }
+  ~bh_scalar_buf() {
+    if (producer.joinable()) producer.join();
+    if (ready) {
+      (void)hipSetDevice(device);
+      (void)hipEventSynchronize(ready);
+      (void)hipEventDestroy(ready);
+    }
+  }
+};
+struct bh_scalars {
+  size_t n = 0;
+  std::shared_ptr<bh_scalar_buf> buf;
 };
 
 struct bh_witness {
@@ -192,6 +252,20 @@ struct bh_ctx {
   bh::H2DRing ring;
   std::unique_ptr<bh::HostPool> pool;
   bh_witness* dropin = nullptr;
+  // bh_compute_h_scalars' producer threads: their own copy stream, pinned ring, memcpy workers and
+  // a|b|c buffer (under bg.mu, one producer at a time), so that an upload in flight never holds
+  // mu; bh_ctx_destroy waits for bg_active == 0
+  struct Background {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    bh::H2DRing ring;
+    std::unique_ptr<bh::HostPool> pool;
+    bh::DevBuf abc;
+    std::atomic<int> fg_uploads{0};  // bh_scalars_upload copies in flight (the producer pauses)
+    std::mutex count_mu;
+    std::condition_variable cv;
+    int active = 0;
+  } bg;
   // bh_multiexp_submit / _wait (jobs.hip): recycled per-job resources under their own lock (a
   // submit never waits behind a proof holding mu)
   std::shared_ptr<bh_job_registry> jobs = std::make_shared<bh_job_registry>();

@@ -310,7 +310,6 @@ inline void shard_range(size_t n, size_t k, size_t N, size_t* lo, size_t* hi) {
 // per (vector, c) -- a function of the CRS only, like Parameters::read -- and cost
 // n * ceil(256/c) points, each padded to whole 128-byte lines so one gather is one (G1)
 // or two (G2) lines (7 GB for a 2^22-point G1 vector at c = 20, 14 GB for b_g2).
-constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use plain windows
 constexpr size_t SMALL_JOB = 4096;                   // run whole on a side stream (latency-bound)
 
 int table_c_for(size_t used_per_shard) {
@@ -338,9 +337,13 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
   const size_t bytes = n * W * rec * 4;
   const size_t chunk = std::min<size_t>(n, (size_t)1 << 19);
   const size_t scratch = g2 ? window_table_scratch_bytes<G2Ops>(chunk, W) : window_table_scratch_bytes<G1Ops>(chunk, W);
-  srs->win.release();
-  srs->win_c = 0;
-  srs->win_lo = srs->win_hi = 0;
+  {
+    // a fresh buffer: multiexp jobs still reading the old table keep it alive until their wait
+    std::lock_guard<std::mutex> lk(srs->win_mu);
+    srs->win = std::make_shared<DevBuf>();
+    srs->win_c = 0;
+    srs->win_lo = srs->win_hi = 0;
+  }
   size_t free_b = 0, total_b = 0;
   BH_TRY_HIP(hipMemGetInfo(&free_b, &total_b));
   if (bytes + scratch + ((size_t)4 << 30) > free_b) {  // keep 4 GB headroom
@@ -350,13 +353,14 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
     srs->skip_c = c; srs->skip_lo = lo; srs->skip_hi = hi;
     return BH_OK;
   }
-  BH_TRY_HIP(srs->win.alloc(bytes));
+  BH_TRY_HIP(srs->win->alloc(bytes));
   DevBuf tmp;
   BH_TRY_HIP(tmp.alloc(scratch));
   const uint32_t* pts = srs->pts.as<uint32_t>() + lo * (g2 ? 48 : 24);
-  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
-  else BH_TRY_HIP(window_table<G1Ops>(pts, n, c, W, srs->win.as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
+  if (g2) BH_TRY_HIP(window_table<G2Ops>(pts, n, c, W, srs->win->as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
+  else BH_TRY_HIP(window_table<G1Ops>(pts, n, c, W, srs->win->as<uint32_t>(), rec, tmp.p, chunk, ctx->stream));
   BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  std::lock_guard<std::mutex> lk(srs->win_mu);
   srs->win_c = c;
   srs->win_W = W;
   srs->win_rec = (int)rec;
@@ -1168,7 +1172,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (!use_table[j]) continue;
     bool seen = false;
     for (int q = 0; q < j; q++) seen |= use_table[q] && jobs[q].srs == jobs[j].srs;
-    if (!seen) tb += jobs[j].srs->win.bytes;
+    if (!seen) tb += jobs[j].srs->win->bytes;
   }
   ctx->last_timings[12] = (double)tb;
   drain.ok = true;

@@ -57,6 +57,8 @@ def parse():
                          "(0: skip)")
     ap.add_argument("--c5-log-constraints", type=int, default=20)
     ap.add_argument("--c5-lanes", type=int, default=0, help="bh_prove_batch lanes per GPU (0: library default)")
+    ap.add_argument("--seam", type=int, default=1,
+                    help="with --dropin: also time the multiexp-level seam (bellman_hip.prove_seam)")
     ap.add_argument("--dropin", type=int, default=1,
                     help="also time bh_prove from host buffers (the drop-in path; 1-GPU runs)")
     return ap.parse_args()
@@ -400,6 +402,23 @@ def main():
         t0 = time.perf_counter()
         dropin["proof_verifies"] = bh.verify_proof(vk, ref, public)
         dropin["verify_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        # the multiexp-level seam: the same host buffers through
+        # bh_compute_h_scalars + bh_scalars_upload + eight bh_multiexp_submit_scalars on the
+        # Parameters' vectors + the host assembly, i.e. what a caller swapping only multiexp()
+        # and the H block gets
+        if args.seam:
+            s0 = bh.prove_seam(ctx, params, asg, r, s)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                ps = bh.prove_seam(ctx, params, asg, r, s)
+            ctx.synchronize()
+            sms = (time.perf_counter() - t0) * 1000.0 / args.steps
+            dropin["seam"] = {"value": round(n_constraints / (sms / 1e3), 1), "unit": "constraints/s",
+                              "ms_per_step": round(sms, 3), "vs_dropin": round(dms / sms, 4),
+                              "proof_matches": ps == s0 == ref,
+                              "note": "prove_seam: h on the device, assignments uploaded once, 8 multiexp "
+                                      "jobs on the Parameters' vectors (window tables), host assembly"}
         del asg
     # CPU baseline: rank 0 of a 1-GPU run only (a bounded sample; see cpu_baseline)
     base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints,

@@ -121,6 +121,28 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
                              bh_job** out);
 bh_status bh_multiexp_wait(bh_job* job, uint8_t* out);
 
+/* ---- the same seam on device-resident data.  create_proof clones one Arc<Vec<Fr::Repr>> per
+ * assignment into several multiexps (prover.rs:233-307) and builds h into another
+ * (prover.rs:227-231): a bh_scalars is that Arc on the device -- uploaded once (canonical or
+ * Montgomery words, like bh_multiexp), or produced by bh_compute_h_scalars -- and any number of
+ * multiexps read it.  bh_compute_h_scalars returns at once: a host thread uploads a, b, c and
+ * enqueues the H passes, and multiexps submitted on h meanwhile are enqueued by that thread
+ * behind them, so a caller can submit in create_proof's own order (h first) without waiting.  Freeing the handle
+ * is allowed while multiexps on it are in flight (they keep the device vector until their wait). */
+typedef struct bh_scalars bh_scalars;
+bh_status bh_scalars_upload(bh_ctx* ctx, const uint64_t* exponents, size_t n, int scalar_format, bh_scalars** out);
+bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c,
+                               size_t num_constraints, bh_scalars** h_out);
+size_t bh_scalars_len(const bh_scalars* s);
+bh_status bh_scalars_free(bh_scalars* s);
+/* bh_compute_h_scalars reads a, b, c from a host thread of its own: they stay borrowed until this
+ * returns (or a multiexp on the vector has been waited, or the vector is freed).  Returns the
+ * H block's status (also reported by every multiexp waited on it). */
+bh_status bh_scalars_sync(bh_scalars* s);
+bh_status bh_multiexp_submit_scalars(bh_ctx* ctx, const bh_srs* bases, size_t base_offset,
+                                     const uint64_t* density_words, size_t density_len, const bh_scalars* exps,
+                                     bh_job** out);
+
 /* ---- EvaluationDomain.  Arrays hold 2^log_m Montgomery Fr (4 u64 each), in place. */
 bh_status bh_domain_size(size_t len, size_t* m, uint32_t* log_m);
 bh_status bh_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
@@ -142,6 +164,16 @@ bh_status bh_params_load(bh_ctx* ctx, const uint8_t* bytes, size_t len, int chec
 bh_status bh_params_free(bh_params* p);
 /* sizes: [h, l, a, b_g1, b_g2, ic] */
 bh_status bh_params_sizes(const bh_params* p, size_t out[6]);
+/* ParameterSource::get_h / get_l / get_a / get_b_g1 / get_b_g2 (groth16/mod.rs:414-477): the
+ * Parameters' own base vector as a bh_srs, borrowed (valid while p lives; never bh_srs_free it).
+ * Multiexps over it (bh_multiexp_submit*) use the window tables bh_params_prepare built, as
+ * bh_prove does: the seam then runs at the prover's per-multiexp speed. */
+#define BH_VEC_H 0
+#define BH_VEC_L 1
+#define BH_VEC_A 2
+#define BH_VEC_B_G1 3
+#define BH_VEC_B_G2 4
+bh_status bh_params_vector(const bh_params* p, int which, const bh_srs** out);
 
 /* ---- prover (create_proof after synthesis, prover.rs:206-349) */
 /* a,b,c: num_constraints Montgomery Fr (ProvingAssignment a/b/c incl. the input constraints);

@@ -798,3 +798,92 @@ def test_two_contexts_share_one_parameters(ctx):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("rounds", [15, 5000, (1 << 15) - 1, (1 << 17) - 1])
+def test_multiexp_seam_proof_equals_prove(ctx, golden, rounds):
+    """INTEGRATION.md section 2's swap at the multiexp level (multiexp.rs:252-281 inside
+    create_proof, prover.rs:206-349): h computed on the device (bh_compute_h_scalars), the
+    assignments uploaded once as bh_scalars, the eight multiexps submitted on the Parameters' own
+    vectors (bh_params_vector, so the window tables bh_params_prepare built are used from 2^16
+    set scalars up) and assembled by bh_proof_from_partials: byte-equal to bh_prove."""
+    bh = _bh()
+    params = bh.Parameters.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    want = bh.prove(ctx, params, asg, 27134, 17146)
+    if rounds >= (1 << 15) - 1:
+        params.prepare(bh.Witness.chain(ctx, rounds))
+    assert bh.prove_seam(ctx, params, asg, 27134, 17146) == want
+    if rounds == 15:
+        fx = [f for f in golden["proofs"] if f["name"] == "mimc_chain_r15"][0]
+        assert want.hex() == fx["proof"]
+
+
+def test_scalars_outlive_their_handle(ctx):
+    """A multiexp in flight keeps the device vector it reads: the bh_scalars freed right after
+    submit still gives the result of a fresh run (and of the host-buffer multiexp)."""
+    bh = _bh()
+    rounds = (1 << 17) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    params.prepare(bh.Witness.chain(ctx, rounds))
+    asg = bh.chain_assignment(rounds)
+    L = params.vector(bh.BH_VEC_L)
+    aux = bh.Scalars(ctx, asg["aux"], montgomery=True)
+    want = bh.multiexp_async(ctx, L, 0, None, aux).wait()
+    w = bh.multiexp_async(ctx, L, 0, None, aux)
+    aux.close()
+    assert w.wait() == want
+    assert bh.multiexp(ctx, L, 0, None, asg["aux"], montgomery=True) == want
+    assert bh.multiexp_async(ctx, L, 0, None, asg["aux"], montgomery=True).wait() == want
+
+
+def test_h_scalars_deferred_submit_and_context_teardown(ctx):
+    """Multiexps submitted on h while bh_compute_h_scalars' producer is still uploading are
+    enqueued by that producer (create_proof's order: h first); a context destroyed with such
+    jobs pending waits for the producer, then detaches them (wait raises)."""
+    bh = _bh()
+    rounds = (1 << 15) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    H = params.vector(bh.BH_VEC_H)
+    h = bh.compute_h_scalars(ctx, asg["a"], asg["b"], asg["c"])
+    ws = [bh.multiexp_async(ctx, H, 0, None, h) for _ in range(3)]
+    got = [w.wait() for w in ws]
+    h.sync()
+    assert got[0] == got[1] == got[2]
+    hv = bh.compute_h(ctx, asg["a"], asg["b"], asg["c"])
+    assert len(h) == len(hv)
+    assert bh.multiexp(ctx, H, 0, None, hv) == got[0]
+    c2 = bh.Context(0)
+    p2 = bh.Parameters.chain(c2, rounds)
+    h2 = bh.compute_h_scalars(c2, asg["a"], asg["b"], asg["c"])
+    w2 = bh.multiexp_async(c2, p2.vector(bh.BH_VEC_H), 0, None, h2)
+    c2.close()
+    with pytest.raises(bh.SynthesisError):
+        w2.wait()
+    h2.close()
+
+
+def test_shared_sorts_follow_the_vector_not_its_address(ctx):
+    """Jobs over the same bh_scalars vector, density map, base offset and digit geometry
+    (b_g1_aux and b_g2_aux) share one digit sort; a vector freed and replaced by another with
+    other contents (likely at the same device address) is sorted afresh: every result equals the
+    host-buffer multiexp."""
+    bh = _bh()
+    rounds = (1 << 15) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    params.prepare(bh.Witness.chain(ctx, rounds))
+    asg = bh.chain_assignment(rounds)
+    ni, na = asg["inputs"].shape[0], asg["aux"].shape[0]
+    B1, B2 = params.vector(bh.BH_VEC_B_G1), params.vector(bh.BH_VEC_B_G2)
+    dens = bh.DensityWords(asg["b_aux_density"], na)
+    off = bh.DensityWords(asg["b_input_density"], ni).total()
+    for k in range(3):
+        ex = np.ascontiguousarray(np.roll(asg["aux"], 977 * k, axis=0))
+        v = bh.Scalars(ctx, ex, montgomery=True)
+        w1 = bh.multiexp_async(ctx, B1, off, dens, v)
+        w2 = bh.multiexp_async(ctx, B2, off, dens, v)
+        got = (w1.wait(), w2.wait())
+        v.close()
+        assert got == (bh.multiexp(ctx, B1, off, dens, ex, montgomery=True),
+                       bh.multiexp(ctx, B2, off, dens, ex, montgomery=True))
