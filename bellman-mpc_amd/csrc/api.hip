@@ -800,6 +800,37 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   return BH_OK;
 }
 
+// A context that borrows every stream of `primary` (bh_prove_batch's pipelined lanes): its own
+// workspaces, events and pinned buffers, so a second proof can be enqueued while the first
+// one's tails run, and no hardware queue more -- the streams' order is the pipeline.
+__attribute__((visibility("hidden"))) bh_status ctx_create_lane(bh_ctx* primary, bh_ctx** out) {
+  bh_ctx* c = new bh_ctx();
+  c->device = primary->device;
+  c->borrowed_streams = true;
+  c->stream = primary->stream;
+  c->stream2 = primary->stream2;
+  c->stream3 = primary->stream3;
+  c->stream4 = primary->stream4;
+  c->stream4d = primary->stream4d;
+  c->h2d = primary->h2d;
+  for (int q = 0; q < bh_ctx::TAIL_STREAMS; q++) c->tstream[q] = primary->tstream[q];
+  c->tables = primary->tables;
+  c->window_override = primary->window_override;
+  bool ok = true;
+  for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  for (auto& e : c->jev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  ok = ok && hipHostMalloc(&c->host_out1, 8 * 128 * sizeof(XYZZ<G1F>), hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc(&c->host_out2, 2 * 128 * sizeof(XYZZ<Fp2Ops>), hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc(&c->host_counts, 32 * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess &&
+       hipHostMalloc(&c->host_spans, 8 * MAX_SPAN_BLOCKS * sizeof(uint32_t), hipHostMallocDefault) == hipSuccess;
+  if (!ok) {
+    bh_ctx_destroy(c);
+    return BH_ERR_OUT_OF_MEMORY;
+  }
+  *out = c;
+  return BH_OK;
+}
+
 bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (!ctx) return BH_OK;
   for (bh_ctx* v : ctx->vranks) bh_ctx_destroy(v);
@@ -833,13 +864,15 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   if (ctx->host_out2) (void)hipHostFree(ctx->host_out2);
   if (ctx->host_counts) (void)hipHostFree(ctx->host_counts);
   if (ctx->host_spans) (void)hipHostFree(ctx->host_spans);
-  (void)hipStreamDestroy(ctx->stream);
-  if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
-  (void)hipStreamDestroy(ctx->stream2);
-  (void)hipStreamDestroy(ctx->stream3);
-  (void)hipStreamDestroy(ctx->stream4);
-  if (ctx->stream4d) (void)hipStreamDestroy(ctx->stream4d);
-  for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
+  if (!ctx->borrowed_streams) {
+    (void)hipStreamDestroy(ctx->stream);
+    if (ctx->h2d) (void)hipStreamDestroy(ctx->h2d);
+    (void)hipStreamDestroy(ctx->stream2);
+    (void)hipStreamDestroy(ctx->stream3);
+    (void)hipStreamDestroy(ctx->stream4);
+    if (ctx->stream4d) (void)hipStreamDestroy(ctx->stream4d);
+    for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
+  }
   release_mask(ctx);
   delete ctx->dist;
   delete ctx;

@@ -207,6 +207,7 @@ struct bh_witness {
 struct bh_ctx {
   int device = 0;
   bool cu_masked = false;  // its tail streams are CU-masked (the first live context of a device)
+  bool borrowed_streams = false;  // a pipelined batch lane: the streams are its primary's (ctx_create_lane)
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
@@ -273,6 +274,7 @@ struct bh_ctx {
 };
 
 void bh_ctx_release_jobs(bh_ctx* ctx);
+extern "C" bh_status ctx_create_lane(bh_ctx* primary, bh_ctx** out);  // (defined in api.hip's C block; not exported in the header)
 
 namespace bh {
 bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out);

@@ -23,7 +23,7 @@ using namespace bh;
 struct bh_job_slot {
   hipEvent_t uploaded = nullptr, sorted = nullptr, accumulated = nullptr, done = nullptr;
   uint64_t use = 0;  // bumped each time the slot is taken (bh_job_registry::SortRec validity)
-  DevBuf raw, scalars, dwords, idx, dtmp, dscan;
+  DevBuf raw, scalars, dwords, idx, dtmp, dscan, dspan;
   MsmWorkspace<G1Ops> ws1;
   MsmWorkspace<G2Ops> ws2;
   ~bh_job_slot() {  // (its last use was waited for, or the context's streams were drained)
@@ -175,12 +175,16 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
       if (reg.sorts.size() > 16) reg.sorts.erase(reg.sorts.begin());
     }
   }
+  // the longest bucket span, read on the device by the tail (no host wait before its enqueue)
+  const size_t nbt = (size_t)job->sh.Wb * job->sh.NB;
+  BH_TRY_HIP(sl->dspan.alloc(MAX_SPAN_BLOCKS * 4));
+  BH_TRY_HIP(max_span(ws.counts, ws.offsets, nbt, (uint32_t)job->sh.S, sl->dspan.as<uint32_t>(), nullptr, st.sort));
   BH_TRY_HIP(hipEventRecord(sl->sorted, st.sort));
   BH_TRY_HIP(hipStreamWaitEvent(st.acc, sl->sorted, 0));
   BH_TRY_HIP(msm_accumulate<C>(ws, st.acc, pts, n, job->sh, nullptr));
   BH_TRY_HIP(hipEventRecord(sl->accumulated, st.acc));
   BH_TRY_HIP(hipStreamWaitEvent(st.tail, sl->accumulated, 0));
-  BH_TRY_HIP(msm_back<C>(ws, st.tail, n, job->sh, ws.host_window_sums));
+  BH_TRY_HIP(msm_back<C>(ws, st.tail, n, job->sh, ws.host_window_sums, -1, nullptr, sl->dspan.as<uint32_t>()));
   BH_TRY_HIP(hipEventRecord(sl->done, st.tail));
   return BH_OK;
 }

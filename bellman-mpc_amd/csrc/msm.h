@@ -108,9 +108,12 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 // -1: every level a bucket could need
 // halves: the caller orders `st` after the lower half (MsmTiming::ev_half); msm_back enqueues
 // the lower half's reduction, waits for `acc_done` (the whole accumulation), then the upper's
+// d_span_words (with max_span = -1): max_span()'s device words for this multiexp -- the kernels
+// read the longest span themselves (fold in the reduction up to 8 segments, else k_cont_seq),
+// so the host need not wait for the sort before enqueueing the tail
 template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
-                    int max_span = -1, hipEvent_t acc_done = nullptr);
+                    int max_span = -1, hipEvent_t acc_done = nullptr, const uint32_t* d_span_words = nullptr);
 
 size_t scan_scratch_words(size_t n);
 // max over buckets of (last segment - first segment) for segment length S: the

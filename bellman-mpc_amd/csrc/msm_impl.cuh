@@ -112,16 +112,37 @@ inline size_t cont_seq_max() {
   return v;
 }
 
+// Max over the g per-workgroup words k_max_span wrote (msm_common.hip): the longest bucket span,
+// read by every workgroup of the kernels below when the host has not read it (device-decided
+// tails: no host wait between a multiexp's sort and the enqueue of its tail).  Block-uniform.
+__device__ __forceinline__ uint32_t block_span(const uint32_t* words, uint32_t g) {
+  __shared__ uint32_t red[4];
+  uint32_t m = 0;
+  for (uint32_t i = threadIdx.x; i < g; i += blockDim.x) m = max(m, words[i]);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = red[0];
+  for (uint32_t w = 1; w < (blockDim.x + 63) / 64; w++) m = max(m, red[w]);
+  __syncthreads();  // (red is reused by the next call)
+  return m;
+}
+
 // The same fold for buckets spanning at most cont_seq_max() segments, Q threads per bucket:
 // thread q of bucket b sums the partials i = q, q+Q, q+2Q, ... of conts[s_first+1 ..
 // s_last], then the Q sums meet in LDS (log2(Q) more additions), so a bucket spanning 16
 // segments costs 4 + 2 serial additions instead of 15.  The tails are VALU-bound chains
 // on a small fraction of the SIMDs: serial depth is their latency.
+// span_words != null (device-decided): the whole grid returns when the longest span is at most
+// fold_span (k_reduce_blocks folds those), and otherwise folds every span, however long.
 template <class C, int Q>
 __global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
-                                                  uint32_t nbr, uint32_t S, typename C::P* conts) {
+                                                  uint32_t nbr, uint32_t S, typename C::P* conts,
+                                                  const uint32_t* span_words, uint32_t span_g, uint32_t fold_span) {
   extern __shared__ uint4 lds_raw[];
   typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  if (span_words && block_span(span_words, span_g) <= fold_span) return;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t b = b0 + gid / Q, q = gid % Q;  // buckets [b0, b0 + nbr)
   uint32_t s_first = 0, ncont = 0;
@@ -234,9 +255,11 @@ template <class C>
 __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
                                                        const typename C::P* bucket_sums, const typename C::P* conts,
                                                        uint32_t S, uint32_t b0, uint32_t NB, uint32_t L, int lgL,
-                                                       uint32_t nblk, int fold, typename C::P* Y, typename C::P* Ssum) {
+                                                       uint32_t nblk, int fold, typename C::P* Y, typename C::P* Ssum,
+                                                       const uint32_t* span_words, uint32_t span_g, uint32_t fold_span) {
   extern __shared__ uint4 lds_raw[];
   typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  if (span_words) fold = block_span(span_words, span_g) <= fold_span ? 1 : 0;  // device-decided
   const uint32_t i = threadIdx.x;
   const uint32_t w = blockIdx.x / nblk, blk = blockIdx.x % nblk;
   const uint32_t gb0 = b0 + w * NB + (blk * blockDim.x + i) * L;
@@ -614,18 +637,24 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 
 // Reduction of the buckets [b0, b0 + nbr) of each of Wb windows (window stride NB): continuation
 // fix-up, then the two-level summation by parts into out[] (Wb totals, or 3 points when split).
+struct SpanSrc {  // device-decided tails: k_max_span's words (null: the host decided)
+  const uint32_t* words = nullptr;
+  uint32_t g = 0, fold_span = 0;
+};
+
 template <class C>
 static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, size_t segs, size_t span,
                          bool fold, bool seq, uint32_t b0, uint32_t nbr, uint32_t L, uint32_t y_off,
-                         typename C::P* out) {
+                         typename C::P* out, const SpanSrc& dev = SpanSrc()) {
   constexpr bool G2 = sizeof(typename C::P) > 256;
   const size_t nb_all = (size_t)sh.Wb * nbr;
-  if (!fold && seq) {
+  if (dev.words || (!fold && seq)) {
     constexpr int Q = 4;
     constexpr uint32_t B = G2 ? 128 : 256;  // LDS: B points
-    if (span >= 2)
+    if (dev.words || span >= 2)
       hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nb_all * Q, B)), dim3(B), B * sizeof(typename C::P),
-                         st, ws.counts, ws.offsets, b0, (uint32_t)nb_all, (uint32_t)sh.S, ws.conts);
+                         st, ws.counts, ws.offsets, b0, (uint32_t)nb_all, (uint32_t)sh.S, ws.conts, dev.words, dev.g,
+                         dev.fold_span);
   } else if (!fold) {
     const size_t nbt = (size_t)sh.Wb * sh.NB;
     for (size_t stride = 1; stride < span; stride *= 4)
@@ -643,7 +672,8 @@ static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh
   const int split = sh.Wb == 1 ? 1 : 0;
   hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
                      ws.counts, ws.offsets, ws.bucket_sums, ws.conts, (uint32_t)sh.S, b0, (uint32_t)sh.NB, L,
-                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted + y_off, ws.seg_sum + y_off);
+                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted + y_off, ws.seg_sum + y_off, dev.words, dev.g,
+                     dev.fold_span);
   hipLaunchKernelGGL(k_reduce_window<C>, dim3((unsigned)sh.Wb), dim3(BT2), 2 * BT2 * sizeof(typename C::P), st,
                      ws.seg_weighted + y_off, ws.seg_sum + y_off, nblk, Lb, reduce_lg2(Lb),
                      reduce_lg2(L) + reduce_lg2(BT), split, out);
@@ -653,7 +683,7 @@ static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh
 // (Wb entries; 2 for one shared window; 6 for halves, see reduce_halves_shift).
 template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
-                    int max_span, hipEvent_t acc_done) {
+                    int max_span, hipEvent_t acc_done, const uint32_t* d_span_words) {
   // continuation partials: a bucket spanning up to REDUCE_FOLD_SPAN segments has them added
   // by its reduction thread (no extra launch); longer spans (known from the sort) are folded
   // first -- Q threads per bucket, or log-depth 4-ary tree levels
@@ -665,16 +695,22 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
   const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;
   const bool seq = max_span >= 0 && span <= cont_seq_max();
+  SpanSrc dev;
+  if (max_span < 0 && d_span_words) {  // device-decided: fold up to REDUCE_FOLD_SPAN, else k_cont_seq
+    dev.words = d_span_words;
+    dev.g = max_span_blocks((size_t)sh.Wb * sh.NB);
+    dev.fold_span = (uint32_t)REDUCE_FOLD_SPAN;
+  }
   if (sh.halves) {
     const uint32_t nbh = (uint32_t)sh.NB / 2;
-    reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums);
+    reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums, dev);
     if (acc_done) hipStreamWaitEvent(st, acc_done, 0);
     const uint32_t y_off = nbh / sh.L / reduce_threads_for(nbh, (uint32_t)sh.L, sizeof(typename C::P) > 256);
-    reduce_range<C>(ws, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3);
+    reduce_range<C>(ws, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3, dev);
     hipMemcpyAsync(host_out, ws.window_sums, 6 * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
     return hipGetLastError();
   }
-  reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums);
+  reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums, dev);
   hipMemcpyAsync(host_out, ws.window_sums, (sh.Wb == 1 ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost,
                  st);
   return hipGetLastError();

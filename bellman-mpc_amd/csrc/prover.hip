@@ -627,6 +627,14 @@ bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t n
 
 // `shard` of `nshards`: res1 = [h, l, a_inputs, a_aux, b_g1_inputs, b_g1_aux],
 // res2 = [b_g2_inputs, b_g2_aux].  Error checks cover the full (unsharded) query.
+// bh_prove_batch's pipelined lanes (set by the lane thread around one proof): after_accs once
+// the proof has enqueued everything but its reduction tails, before_tails / after_tails around
+// the tails' enqueue (proof order on the shared tail streams)
+struct LaneHooks {
+  std::function<void()> after_accs, before_tails, after_tails;
+};
+thread_local LaneHooks t_lane;
+
 bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w, size_t shard, size_t nshards,
                        Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
                        UploadSync* up = nullptr) {
@@ -702,8 +710,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated,
                                // [32] start, [33] density maps ready
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
-  BH_TRY_HIP(hipStreamWaitEvent(sS, jev[32], 0));
-  BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
+  // ordered after whatever this context ran before on its main stream -- except on a pipelined
+  // batch lane (borrowed streams): there the main stream holds the previous proof's
+  // accumulations, which this proof's density maps and sorts must not wait for (they read only
+  // this lane's own witness and workspaces)
+  if (!ctx->borrowed_streams) {
+    BH_TRY_HIP(hipStreamWaitEvent(sS, jev[32], 0));
+    BH_TRY_HIP(hipStreamWaitEvent(sT, jev[32], 0));
+  }
 
   // ---- the 8 multiexps (prover.rs:233-307)
   BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
@@ -953,15 +967,31 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
     BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
                               hipMemcpyDeviceToHost, st));
+    // The longest bucket span picks the continuation fold.  Default: the tail kernels read the
+    // sort's span words on the device, so enqueueing a tail never waits for its sort (a pipelined
+    // batch hands the streams on to the next proof without waiting for this one's h sort, which
+    // follows H).  BH_TAIL_HOST_SPAN=1: the host reads it once the sort is done (round 2 scheme;
+    // it also skips k_cont_seq's launch when the spans are short).
+    static const bool host_span = [] {
+      const char* e = getenv("BH_TAIL_HOST_SPAN");
+      return e && e[0] == '1';
+    }();
     int span = -1;
-    if (n >= SMALL_JOB) {  // the sort ran ahead; its span word is on the host once it is done
-      BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
-      span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS, (size_t)shapes[j].Wb * shapes[j].NB);
+    const uint32_t* dspan = nullptr;
+    if (n >= SMALL_JOB) {
+      if (host_span) {
+        BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
+        span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS, (size_t)shapes[j].Wb * shapes[j].NB);
+      } else {
+        dspan = ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS;
+      }
     }
     if (J.g2)
-      BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span, jev[24 + j]));
+      BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span, jev[24 + j],
+                                 dspan));
     else
-      BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span, jev[24 + j]));
+      BH_TRY_HIP(msm_back<G1Ops>(ctx->pw1[J.out], st, n, shapes[j], ctx->host_out1 + 128 * J.out, span, jev[24 + j],
+                                 dspan));
     return BH_OK;
   };
   BH_TRY_HIP(hipEventRecord(jev[33], sS));
@@ -1054,6 +1084,16 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // Sort order = accumulation order (b_g2_aux sorted, b_g1_aux copied, l sorted, a_aux
   // compacted from l, h): putting l first so that b_g2_aux could be compacted from it would
   // lengthen the start-up (measured +2 ms at 2^22), so only later sorts are derived.
+  // h's digit sort reads the H block's output: on a replicated H it runs on the H stream right
+  // behind it, so the sort stream never waits for H (a pipelined batch's next proof queues its
+  // density maps and sorts there, behind this proof's); distributed H (CU-masked stream) keeps it
+  // on the sort stream after an event wait
+  auto sort_h_or = [&](int j) -> bh_status {
+    if (!jobs[j].is_h) return sort_job(j, sS);
+    if (!dh) return sort_job(j, sH);
+    BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
+    return sort_job(j, sS);
+  };
   int sorder[8];
   const int ns = nbig;
   for (int q = 0; q < nbig; q++) sorder[q] = big[q];
@@ -1069,8 +1109,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
 
   for (int r = 0; r < pre_sorts; r++) {
-    if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    if ((s = sort_job(sorder[r], sS))) return s;
+    if ((s = sort_h_or(sorder[r]))) return s;
   }
   if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
   // 4 = enqueued between the first sorts and the first accumulation: the sorts are not held up
@@ -1091,17 +1130,32 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (h_mode == 3 && (s = enqueue_h(jev[33]))) return s;
   const auto t_h = std::chrono::steady_clock::now();
   for (int r = pre_sorts; r < ns; r++) {
-    if (jobs[sorder[r]].is_h) BH_TRY_HIP(hipStreamWaitEvent(sS, ctx->ev[1], 0));
-    if ((s = sort_job(sorder[r], sS))) return s;
+    if ((s = sort_h_or(sorder[r]))) return s;
   }
   const auto t_sorts = std::chrono::steady_clock::now();
   for (int q = 1; q < nbig; q++)
     if ((s = acc_job(big[q], sA))) return s;
   if (nbig > 0) last_acc = big[nbig - 1];
   if ((s = run_small())) return s;
-  for (int q = 0; q < nbig; q++)
+  // The host waits below are on events of THIS proof's work (not stream syncs): on a pipelined
+  // batch lane the streams soon hold the next proof's work behind it.
+  // ev[10..13]: small multiexps, sorts, accumulations, H; ev[2+q]: tail q
+  BH_TRY_HIP(hipEventRecord(ctx->ev[10], sT));
+  BH_TRY_HIP(hipEventRecord(ctx->ev[11], sS));
+  BH_TRY_HIP(hipEventRecord(ctx->ev[12], sA));
+  BH_TRY_HIP(hipEventRecord(ctx->ev[13], sH));
+  // pipelined batch lanes: the next proof may enqueue its start-up and accumulations now (they
+  // queue behind these on every stream); this proof's tails go in only after the previous
+  // proof's (a tail stream would otherwise hold them behind the next proof's tails)
+  const auto t_hand = std::chrono::steady_clock::now();
+  if (t_lane.after_accs) t_lane.after_accs();
+  if (t_lane.before_tails) t_lane.before_tails();
+  for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
+    BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
+  }
   const auto t_enq = std::chrono::steady_clock::now();
+  if (t_lane.after_tails) t_lane.after_tails();
   float g1_acc_ms = 0, g2_acc_ms = 0;
   size_t g1_pairs = 0, g2_pairs = 0, g1_adds = 0, g2_adds = 0;
   int g1_launches = 0, g2_launches = 0;
@@ -1116,8 +1170,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   for (int o = 0; o < nord; o++) {
     const int j = order[o];
     const Job& J = jobs[j];
-    if (o == 0 || o == nsmall) BH_TRY_HIP(hipStreamSynchronize(sT));
-    if (o >= nsmall) BH_TRY_HIP(hipStreamSynchronize(tails[o - nsmall]));
+    if (o == 0 || o == nsmall) BH_TRY_HIP(hipEventSynchronize(ctx->ev[10]));
+    if (o >= nsmall) BH_TRY_HIP(hipEventSynchronize(ctx->ev[2 + (o - nsmall)]));
     float t = 0;
     if (acc_events_on()) (void)hipEventElapsedTime(&t, jev[2 * j], jev[2 * j + 1]);
     const size_t pairs = (size_t)((unsigned __int128)J.used * (his[j] - los[j]) / std::max<size_t>(J.n, 1));
@@ -1129,10 +1183,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       g1_acc_ms += t; g1_launches++; g1_pairs += pairs; g1_adds += ctx->host_counts[j];
     }
   }
-  BH_TRY_HIP(hipStreamSynchronize(sS));
-  BH_TRY_HIP(hipStreamSynchronize(sA));
-  BH_TRY_HIP(hipStreamSynchronize(sH));
-  BH_TRY_HIP(hipStreamSynchronize(sT));
+  for (int e = 10; e <= 13; e++) BH_TRY_HIP(hipEventSynchronize(ctx->ev[e]));
   if (host_in) {
     hin.th.join();
     if (hin.st) return hin.st;
@@ -1148,8 +1199,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    fprintf(stderr, "compute_msms host: first accumulation enqueued %.3f ms, H %.3f, sorts %.3f, enqueue done %.3f, gpu and combines done %.3f, after %.3f\n",
-            ms(t0, t_acc0), ms(t0, t_h), ms(t0, t_sorts), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
+    fprintf(stderr, "compute_msms host: ctx %p start %.3f ms (monotonic), first accumulation enqueued %.3f ms, H %.3f, sorts %.3f, accumulations handed on %.3f, enqueue done %.3f, gpu and combines done %.3f, after %.3f\n",
+            (void*)ctx, std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), ms(t0, t_acc0), ms(t0, t_h),
+            ms(t0, t_sorts), ms(t0, t_hand), ms(t0, t_enq), ms(t0, t_gpu), ms(t_gpu, t1));
   }
   float h_ms = 0;
   hipEventElapsedTime(&h_ms, ctx->ev[0], ctx->ev[1]);
@@ -1544,6 +1596,16 @@ bh_status bh_rehearse_rank(bh_ctx* ctx, const bh_params* params, const bh_witnes
   return BH_OK;
 }
 
+// default pipelined lanes of bh_prove_batch (BH_BATCH_LANES: A/B experiments)
+static int batch_lanes() {
+  static const int v = [] {
+    const char* e = getenv("BH_BATCH_LANES");
+    const int x = e ? atoi(e) : 2;
+    return (x >= 1 && x <= 16) ? x : 2;
+  }();
+  return v;
+}
+
 bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
                          const uint64_t r_in[4], const uint64_t s_in[4], int lanes, uint8_t* proofs_out) {
   if (!ctx || !params || !ws || !r_in || !s_in || !proofs_out || lanes < 0 || lanes > 16) return BH_ERR_INVALID_ARGUMENT;
@@ -1557,12 +1619,11 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
   // on `lanes` contexts of this device, each driven by a host thread through a share of the
   // batch, so one proof's start-up (sorts, H) and reduction tails fill the bubbles of
   // another's accumulations; proofs_out[i] is exactly bh_prove_witness(ws[i]).
-  const int L = (int)std::min<size_t>(lanes ? (size_t)lanes : 1, k);
+  // lanes = 0: the default, BATCH_LANES pipelined lanes
+  const int L = (int)std::min<size_t>(lanes ? (size_t)lanes : (size_t)batch_lanes(), k);
   if (L == 1) {
-    // one lane: the proofs back to back on this context.  A proof already fills the device
-    // (same-box A/B at 2^20: 19.7 ms per proof with one lane, 19.8 with two, 21.6 with three),
-    // and every extra context adds 13 streams, i.e. hardware queues: beyond the 16 the library
-    // asks for, queues time-share and a proof takes ~33 ms.
+    // one lane: the proofs back to back on this context, each one's start-up and last tail
+    // exposed (2^20 proofs: 17.98 ms each, BENCH r03 before the pipelined lanes)
     // r and s are shared by the batch: their terms of A, B, C once, beside the first proof
     AssemblePreThread pre(vk_of(params), r_in, s_in);
     for (size_t i = 0; i < k; i++) {
@@ -1574,9 +1635,17 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
     }
     return BH_OK;
   }
+  // Pipelined lanes (the reference's Worker::compute fan-out, multicore.rs:33-76): L contexts that
+  // borrow THIS context's streams (ctx_create_lane: own workspaces, events and buffers, no extra
+  // hardware queue), driven by L host threads that take turns in proof order.  Proof i+1 is
+  // enqueued as soon as proof i's device work is (t_enqueued_hook), so its density maps, sorts and
+  // H sit in the streams behind proof i's accumulations and run beside proof i's last reduction
+  // tail and host combine; stream order keeps the accumulations proof after proof.
+  // (Round 2's lanes were contexts with streams of their own: 19.8 ms per 2^20 proof with two,
+  // slower than one lane -- every extra context added 13 streams to the queue budget.)
   while ((int)ctx->lanes.size() < L) {
     bh_ctx* v = nullptr;
-    bh_status st = bh_ctx_create(ctx->device, &v);
+    bh_status st = ctx_create_lane(ctx, &v);
     if (st) return st;
     ctx->lanes.push_back(v);
   }
@@ -1599,18 +1668,60 @@ bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness*
     }
   }
   const AssemblePre pre = assemble_pre(vk_of(params), r_in, s_in);
+  // two turnstiles in proof order: turn[0] = the next proof allowed to start enqueueing, turn[1] =
+  // the next proof allowed to enqueue its reduction tails
+  std::mutex turn_mu;
+  std::condition_variable turn_cv;
+  size_t turn[2] = {0, 0};
+  std::atomic<bool> failed{false};
+  auto pass = [&](int t, size_t i) {
+    {
+      std::lock_guard<std::mutex> lk(turn_mu);
+      if (turn[t] == i) turn[t] = i + 1;
+    }
+    turn_cv.notify_all();
+  };
+  auto await = [&](int t, size_t i) {
+    std::unique_lock<std::mutex> lk(turn_mu);
+    turn_cv.wait(lk, [&] { return turn[t] == i; });
+  };
+  // proof i is over on this lane: both turns handed on (no-ops where its hooks already did;
+  // an early error still hands the tail turn on after the previous proof's, in order)
+  auto close = [&](size_t i) {
+    {
+      std::unique_lock<std::mutex> lk(turn_mu);
+      if (turn[0] == i) turn[0] = i + 1;
+      turn_cv.notify_all();
+      turn_cv.wait(lk, [&] { return turn[1] >= i; });
+      if (turn[1] == i) turn[1] = i + 1;
+    }
+    turn_cv.notify_all();
+  };
   std::vector<bh_status> st(L, BH_OK);
   std::vector<std::thread> th;
   for (int l = 0; l < L; l++)
     th.emplace_back([&, l] {
       bh_ctx* v = ctx->lanes[l];
       std::lock_guard<std::mutex> vl(v->mu);
-      if (hipSetDevice(v->device) != hipSuccess) { st[l] = BH_ERR_HIP; return; }
+      if (hipSetDevice(v->device) != hipSuccess) st[l] = BH_ERR_HIP;
       for (size_t i = (size_t)l; i < k; i += (size_t)L) {
+        await(0, i);
+        if (st[l] || failed) {  // a failed lane still passes its turns: no thread waits forever
+          close(i);
+          continue;
+        }
+        t_lane.after_accs = [&pass, i] { pass(0, i); };
+        t_lane.before_tails = [&await, i] { await(1, i); };
+        t_lane.after_tails = [&pass, i] { pass(1, i); };
         Jac<Fp> r1[6];
         Jac<bh::Fp2> r2[2];
         st[l] = compute_msms_sync(v, params, ws[i], 0, 1, r1, r2, nullptr, false);
-        if (st[l]) return;
+        t_lane = LaneHooks();
+        close(i);
+        if (st[l]) {
+          failed = true;
+          continue;
+        }
         assemble_finish(pre, r1, r2, proofs_out + 192 * i);
       }
     });

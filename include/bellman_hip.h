@@ -203,12 +203,13 @@ bh_status bh_prove_witness(bh_ctx* ctx, const bh_params* params, const bh_witnes
 
 /* Throughput mode (BASELINE.json configs[4], "C5"): k independent proofs of witnesses sharing
  * one Parameters (the reference's Worker::compute fan-out, multicore.rs:33-76, r and s fixed,
- * prover.rs:158-173), every window table built once up front.  lanes (0 = default, 1): with 1
- * the proofs run back to back on ctx (a 2^20 proof already fills the device); with more, on
- * that many contexts of this device driven by host threads, so one proof's sorts, H block and
- * tails overlap another's accumulations (each context adds hardware queues: measured slower).
- * proofs_out: k * 192 bytes, proof i == bh_prove_witness(ws[i]).  Across GPUs the batch is
- * split by the caller (one process per GPU, no collective). */
+ * prover.rs:158-173), every window table built once up front.  lanes (0 = default, 2): with 1
+ * the proofs run back to back on ctx; with L >= 2, L host threads drive L lane contexts that
+ * borrow ctx's streams (no hardware queue more) and take turns in proof order, proof i+1 being
+ * enqueued as soon as proof i's device work is -- its density maps, sorts and H then run beside
+ * proof i's last reduction tail and host combine.  proofs_out: k * 192 bytes, proof i ==
+ * bh_prove_witness(ws[i]).  Across GPUs the batch is split by the caller (one process per GPU,
+ * no collective). */
 bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
                          const uint64_t r[4], const uint64_t s[4], int lanes, uint8_t* proofs_out);
 
