@@ -30,11 +30,11 @@ sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point, scalar)
 G2_PAIR_BYTES = 224
-TRAFFIC_FILE = "r02_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
+TRAFFIC_FILE = "r03_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
 G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X (profiles/r01_curvebench.txt)
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
-PMC_FILE = "r02_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench
+PMC_FILE = "r03_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench
 SOLO_WAVE_INSTR_RATE = 515.0   # G wave-instr/s: the G1 accumulation alone (6.3 G madd/s x 5234 lane-instr / 64)
 
 
@@ -365,9 +365,8 @@ def main():
         with open(ppath) as f:
             pmc = json.load(f)
         per = [v for v in pmc.values() if isinstance(v, dict) and "SQ_INSTS_VALU" in v]
-        g1 = [v for key, v in pmc.items() if key.startswith("k_accumulate_pf<CurveOps<FpOps>")]
-        if per and g1:
-            n_proofs = g1[0]["dispatches"]["SQ_INSTS_VALU"] / 6  # six G1 multiexps per proof
+        if per and pmc.get("proofs"):
+            n_proofs = pmc["proofs"]
             wi = sum(v["SQ_INSTS_VALU"] * v["dispatches"]["SQ_INSTS_VALU"] for v in per) / n_proofs
             rate = wi / (ms / 1e3) / 1e9
             proof_valu = {"wave_instructions_per_proof": round(wi), "achieved": round(rate, 1),
