@@ -1064,7 +1064,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // accumulation's launch; 4 = between the first sorts and the first accumulation.  Round 3,
   // distributed H on its masked half of the CUs, at N = 8 in the one-GPU rehearsal: 1 (default)
   // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
-  // thread 10.44 (not kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
+  // thread 10.44, and H held until the first sorts are done 10.61-10.73 against 10.28-10.37 (neither
+  // kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
   int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 1 : 2);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
