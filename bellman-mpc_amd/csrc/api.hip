@@ -1176,9 +1176,9 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
         uint32_t* dst = abc + (size_t)v * m * 8;
         if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.st));
         if (nc) {
-          // in 32 MB pieces, paused while a bh_scalars_upload streams (the assignments feed the
+          // in 16 MB pieces, paused while a bh_scalars_upload streams (the assignments feed the
           // first sorts; H is needed last)
-          const size_t piece = (size_t)32 << 20;
+          const size_t piece = (size_t)16 << 20;  // one ring slot
           for (size_t off = 0; off < nc * 32; off += piece) {
             while (bg.fg_uploads.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
             BH_TRY_HIP(bg.ring.copy(*bg.pool, reinterpret_cast<uint8_t*>(dst) + off,

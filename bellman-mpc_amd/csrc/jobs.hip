@@ -23,7 +23,7 @@ using namespace bh;
 struct bh_job_slot {
   hipEvent_t uploaded = nullptr, sorted = nullptr, accumulated = nullptr, done = nullptr;
   uint64_t use = 0;  // bumped each time the slot is taken (bh_job_registry::SortRec validity)
-  DevBuf raw, scalars, dwords, idx, dtmp, dscan, dspan;
+  DevBuf raw, scalars, dwords, idx, dtmp, dscan, dscan2, dspan;
   MsmWorkspace<G1Ops> ws1;
   MsmWorkspace<G2Ops> ws2;
   ~bh_job_slot() {  // (its last use was waited for, or the context's streams were drained)
@@ -163,7 +163,31 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
                                sl->dtmp.as<uint32_t>(), sl->dscan.as<uint32_t>(), st.sort));
       d_idx = sl->idx.as<int32_t>();
     }
-    BH_TRY_HIP(msm_sort<C>(ws, st.sort, d_scalars, n, d_idx, (uint32_t)base_offset, job->sh));
+    // a sparser density map over a vector already sorted under FULL density with the same digit
+    // geometry (a_aux and b_g1_aux over l's aux sort): compact those sorted entries through this
+    // map (the prover's derived sort) instead of sorting again
+    bool derived = false;
+    if (st.key && d_idx) {
+      bh_job_registry& reg = *job->reg;
+      std::lock_guard<std::mutex> lk(reg.mu);  // (the source slot cannot be taken again meanwhile)
+      for (const auto& r : reg.sorts) {
+        if (r.scalars_id != st.key || r.dens_hash != 0 || r.n != n || r.c != job->sh.c || r.W != job->sh.W ||
+            r.NB != job->sh.NB || r.Wb != job->sh.Wb || r.pre != job->sh.pre || r.slot->use != r.use || r.slot == sl)
+          continue;
+        const uint32_t *e, *of;
+        if (r.group == BH_G1) { e = r.slot->ws1.entries; of = r.slot->ws1.offsets; }
+        else { e = r.slot->ws2.entries; of = r.slot->ws2.offsets; }
+        BH_TRY_HIP(ws.reserve_shape(n, job->sh));
+        const size_t nbt = (size_t)job->sh.Wb * job->sh.NB, Emax = n * (size_t)job->sh.W;
+        BH_TRY_HIP(sl->dscan2.alloc(derive_scratch_words(Emax) * 4));
+        BH_TRY_HIP(derive_sorted(e, of, nbt, Emax, job->sh.pre, (uint32_t)job->sh.W, (uint32_t)r.base_offset, d_idx,
+                                 reinterpret_cast<uint32_t*>(ws.recs), sl->dscan2.as<uint32_t>(), ws.entries,
+                                 ws.counts, ws.offsets, st.sort));
+        derived = true;
+        break;
+      }
+    }
+    if (!derived) BH_TRY_HIP(msm_sort<C>(ws, st.sort, d_scalars, n, d_idx, (uint32_t)base_offset, job->sh));
     if (st.key) {
       bh_job_registry& reg = *job->reg;
       std::lock_guard<std::mutex> lk(reg.mu);

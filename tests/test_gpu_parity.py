@@ -865,10 +865,11 @@ def test_h_scalars_deferred_submit_and_context_teardown(ctx):
 
 
 def test_shared_sorts_follow_the_vector_not_its_address(ctx):
-    """Jobs over the same bh_scalars vector, density map, base offset and digit geometry
-    (b_g1_aux and b_g2_aux) share one digit sort; a vector freed and replaced by another with
-    other contents (likely at the same device address) is sorted afresh: every result equals the
-    host-buffer multiexp."""
+    """Jobs over the same bh_scalars vector share digit sorts: l's full-density sort is compacted
+    through b_aux's density map for b_g1_aux (the prover's derived sort), and b_g2_aux (same vector,
+    density map, base offset and digit geometry) copies b_g1_aux's; a vector freed and replaced by
+    another with other contents (likely at the same device address) is sorted afresh: every result
+    equals the host-buffer multiexp."""
     bh = _bh()
     rounds = (1 << 15) - 1
     params = bh.Parameters.chain(ctx, rounds)
@@ -876,14 +877,17 @@ def test_shared_sorts_follow_the_vector_not_its_address(ctx):
     asg = bh.chain_assignment(rounds)
     ni, na = asg["inputs"].shape[0], asg["aux"].shape[0]
     B1, B2 = params.vector(bh.BH_VEC_B_G1), params.vector(bh.BH_VEC_B_G2)
+    Lv = params.vector(bh.BH_VEC_L)
     dens = bh.DensityWords(asg["b_aux_density"], na)
     off = bh.DensityWords(asg["b_input_density"], ni).total()
     for k in range(3):
         ex = np.ascontiguousarray(np.roll(asg["aux"], 977 * k, axis=0))
         v = bh.Scalars(ctx, ex, montgomery=True)
+        wl = bh.multiexp_async(ctx, Lv, 0, None, v)
         w1 = bh.multiexp_async(ctx, B1, off, dens, v)
         w2 = bh.multiexp_async(ctx, B2, off, dens, v)
-        got = (w1.wait(), w2.wait())
+        got = (wl.wait(), w1.wait(), w2.wait())
         v.close()
-        assert got == (bh.multiexp(ctx, B1, off, dens, ex, montgomery=True),
+        assert got == (bh.multiexp(ctx, Lv, 0, None, ex, montgomery=True),
+                       bh.multiexp(ctx, B1, off, dens, ex, montgomery=True),
                        bh.multiexp(ctx, B2, off, dens, ex, montgomery=True))
