@@ -6,6 +6,17 @@
 #include "msm.h"
 #include <algorithm>
 
+// Register budget of the kernels a translation unit instantiates: a kernel that runs one wave per
+// SIMD anyway (G2 accumulation, every bucket reduction) may use the whole 512-register file of a
+// lane (256 VGPRs + 256 AGPRs), so the allocator parks values in AGPRs instead of spilling to
+// scratch.  Empty = the compiler's default (G1 accumulation: two waves per SIMD).
+#ifndef BH_ACC_REGS_ATTR
+#define BH_ACC_REGS_ATTR
+#endif
+#ifndef BH_BACK_REGS_ATTR
+#define BH_BACK_REGS_ATTR
+#endif
+
 namespace bh {
 
 static inline unsigned msm_blocks_for(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -80,7 +91,7 @@ __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_
 // partials at j + i*stride, i = 1..F-1 (F-1 serial additions per level instead of one per
 // level of the binary tree).  After the levels with stride < span, conts[s_first+1] holds the sum.
 template <class C, int F>
-__global__ void __launch_bounds__(256) k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
+__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
                                                     const uint32_t* offsets, uint32_t nbt, uint32_t S,
                                                     uint32_t stride, uint32_t b_lo, uint32_t b_hi,
                                                     typename C::P* conts) {
@@ -137,7 +148,7 @@ __device__ __forceinline__ uint32_t block_span(const uint32_t* words, uint32_t g
 // span_words != null (device-decided): the whole grid returns when the longest span is at most
 // fold_span (k_reduce_blocks folds those), and otherwise folds every span, however long.
 template <class C, int Q>
-__global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
+__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
                                                   uint32_t nbr, uint32_t S, typename C::P* conts,
                                                   const uint32_t* span_words, uint32_t span_g, uint32_t fold_span) {
   extern __shared__ uint4 lds_raw[];
@@ -252,7 +263,7 @@ __device__ __forceinline__ void block_epilogue(typename C::P v, const typename C
 // they are all added here (short spans), else k_cont_seq / k_cont_treeF has already folded
 // them into conts[s_first+1].
 template <class C>
-__global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
+__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
                                                        const typename C::P* bucket_sums, const typename C::P* conts,
                                                        uint32_t S, uint32_t b0, uint32_t NB, uint32_t L, int lgL,
                                                        uint32_t nblk, int fold, typename C::P* Y, typename C::P* Ssum,
@@ -323,7 +334,7 @@ __global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, c
 // out[1] = sum_blk blk * S, out[2] = sum_blk S, and the host adds 2^lgM * out[1]
 // (reduce_split_shift; out[2] is the plain bucket sum a bucket range's offset multiplies).
 template <class C>
-__global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
+__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
                                                        uint32_t nblk, uint32_t Lb, int lgLb, int lgM, int split,
                                                        typename C::P* out) {
   extern __shared__ uint4 lds_raw[];
@@ -366,7 +377,7 @@ __global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, c
 // the range keeps the continuation bookkeeping of the whole segment.
 // (A register-load variant without the prefetch measured slower and was removed.)
 template <class C>
-__global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
+__global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
                                                        uint32_t b_lo, uint32_t b_hi, typename C::P* bucket_sums,
                                                        typename C::P* conts, uint32_t* cont_bucket) {
