@@ -10,6 +10,7 @@
 //   k_normalize  : XYZZ -> affine with one inversion per CHUNK points (Montgomery's
 //                  trick), result packed canonical in the bh_srs layout.
 #include "crs.h"
+#include "msm.h"  // G1_TABLE_REC
 
 #include <algorithm>
 
@@ -98,7 +99,7 @@ struct Inv<Fp2Ops> {
 // one thread per CHUNK consecutive points; prefix products kept in `scratch`
 template <class C, int CHUNK>
 __global__ void __launch_bounds__(64) k_normalize(const typename C::P* pts, size_t n, typename FieldOf<C>::F::T* scratch,
-                                                  uint32_t* out_packed, uint32_t rec) {
+                                                  uint32_t* out_packed, uint32_t rec, int limbs) {
   using F = typename FieldOf<C>::F;
   using T = typename F::T;
   constexpr int PW = F::PACKED_WORDS;
@@ -122,8 +123,19 @@ __global__ void __launch_bounds__(64) k_normalize(const typename C::P* pts, size
     // 1/ZZ = ZZZ / z ; 1/ZZZ = ZZ / z
     const T x = F::reduce(F::mul(p.X, F::mul(p.ZZZ, zinv)));
     const T y = F::reduce(F::mul(p.Y, F::mul(p.ZZ, zinv)));
-    F::pack(x, out_packed + i * rec);
-    F::pack(y, out_packed + i * rec + PW);
+    if (limbs) {  // G1 window-table record (G1_TABLE_REC): raw limbs, x then y
+      constexpr int NW = sizeof(T) / 4;
+      const uint32_t* xw = reinterpret_cast<const uint32_t*>(&x);
+      const uint32_t* yw = reinterpret_cast<const uint32_t*>(&y);
+#pragma unroll
+      for (int k = 0; k < NW; k++) {
+        out_packed[i * rec + k] = xw[k];
+        out_packed[i * rec + NW + k] = yw[k];
+      }
+    } else {
+      F::pack(x, out_packed + i * rec);
+      F::pack(y, out_packed + i * rec + PW);
+    }
   }
 }
 
@@ -139,7 +151,7 @@ hipError_t fixed_base_batch(const uint32_t* d_table, const uint32_t* d_scalars, 
   hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st,
                      reinterpret_cast<const P*>(d_xyzz), n,
                      reinterpret_cast<typename FieldOf<C>::F::T*>(d_scratch), d_out,
-                     (uint32_t)(2 * FieldOf<C>::F::PACKED_WORDS));
+                     (uint32_t)(2 * FieldOf<C>::F::PACKED_WORDS), 0);
   return hipGetLastError();
 }
 
@@ -178,7 +190,8 @@ hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t*
     const size_t m = cnt * (size_t)W;
     const size_t threads = (m + CHUNK - 1) / CHUNK;
     hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, xyzz, m,
-                       prefix, d_out + i0 * (size_t)W * rec, rec);
+                       prefix, d_out + i0 * (size_t)W * rec, rec,
+                       (int)(std::is_same<C, G1Ops>::value && rec == G1_TABLE_REC));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -7,6 +7,11 @@
 
 namespace bh {
 
+// Window-table record of a G1 base (one 128-byte line): the affine x and y as 14 + 14 raw 29-bit
+// device limbs (canonical values), so the accumulation reads its operands without unpacking.
+// Plain base vectors stay packed (2 x 12 words); G2 table records are packed in 64 words.
+constexpr uint32_t G1_TABLE_REC = 32;
+
 struct MsmShape {
   int c;    // window bits
   int W;    // digit windows = ceil(256 / c) (signed digits need one spare bit)
@@ -15,7 +20,7 @@ struct MsmShape {
   int S;    // sorted entries per accumulation thread
   int Wb;   // bucket windows: W, or 1 with a window table (all windows share the buckets)
   int pre;  // 1: bases are a window table T[i*W + w] = 2^(c*w) * P_i (entry = i*W + w)
-  int rec;  // u32 words per base record (0: packed affine, 2 x PACKED_WORDS)
+  int rec;  // u32 words per base record (0: packed affine, 2 x PACKED_WORDS; see G1_TABLE_REC)
   // 1 (Wb == 1 only): the bucket set is accumulated and reduced as two halves, each with its own
   // reduction chain, so the lower half's reduction runs beside the upper half's accumulation
   // (the prover's last multiexp, msm_back); L2 = buckets per reduction thread of the upper half

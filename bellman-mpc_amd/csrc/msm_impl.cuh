@@ -23,25 +23,6 @@ static inline unsigned msm_blocks_for(size_t n, unsigned bs) { return (unsigned)
 
 // ----------------------------------------------------------------- accumulate
 template <class C>
-__device__ __forceinline__ typename C::A load_base(const uint32_t* bases, uint32_t e, uint32_t rec) {
-  using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
-  constexpr int PW = F::PACKED_WORDS;
-  const uint32_t idx = e & 0x7fffffffu;
-  const uint4* p = reinterpret_cast<const uint4*>(bases + (size_t)idx * rec);
-  uint32_t w[2 * PW];
-#pragma unroll
-  for (int k = 0; k < PW / 2; k++) {
-    uint4 v = p[k];
-    w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-  }
-  typename C::A a;
-  a.x = F::unpack(w);
-  a.y = F::unpack(w + PW);
-  if (e & 0x80000000u) a = C::neg_affine(a);
-  return a;
-}
-
-template <class C>
 __device__ __forceinline__ void store_point(typename C::P* dst, const typename C::P& p) {
   constexpr int WORDS = sizeof(typename C::P) / 16;
   const uint4* s = reinterpret_cast<const uint4*>(&p);
@@ -383,7 +364,13 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
                                                        typename C::P* conts, uint32_t* cont_bucket) {
   using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
   constexpr int PW = F::PACKED_WORDS;
-  constexpr int NQ = 2 * PW / 4;  // 16-byte pieces per affine base
+  constexpr bool G1 = std::is_same<C, G1Ops>::value;
+  constexpr int NW = sizeof(typename F::T) / 4;    // raw limb words per coordinate (G1: 14)
+  constexpr int NQ = G1 ? NW / 2 : 2 * PW / 4;     // 16-byte pieces per base (G1: up to 7)
+  // G1 window-table records hold raw limbs (G1_TABLE_REC, 7 pieces, no unpacking); plain
+  // vectors are packed (6 pieces)
+  const bool limbs = G1 && rec == G1_TABLE_REC;
+  const int nq = limbs ? NQ : 2 * PW / 4;
   __shared__ uint4 pre[4][NQ][64];
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
@@ -396,8 +383,9 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
     const uint32_t* src = bases + (size_t)(e & 0x7fffffffu) * rec;
 #pragma unroll
     for (int q = 0; q < NQ; q++)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
-                                       (__attribute__((address_space(3))) void*)&pre[wv][q][0], 16, 0, 0);
+      if (q < nq)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
+                                         (__attribute__((address_space(3))) void*)&pre[wv][q][0], 16, 0, 0);
   };
   uint32_t e_cur = entries[start];
   issue(e_cur);
@@ -418,15 +406,25 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
       acc = C::identity();
     }
     __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
-    uint32_t w[2 * PW];
+    uint32_t w[4 * NQ];
 #pragma unroll
     for (int q = 0; q < NQ; q++) {
-      const uint4 v = pre[wv][q][lane];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      if (q < nq) {
+        const uint4 v = pre[wv][q][lane];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      }
     }
     typename C::A a;
-    a.x = F::unpack(w);
-    a.y = F::unpack(w + PW);
+    if (limbs) {
+#pragma unroll
+      for (int k = 0; k < NW; k++) {
+        reinterpret_cast<uint32_t*>(&a.x)[k] = w[k];
+        reinterpret_cast<uint32_t*>(&a.y)[k] = w[NW + k];
+      }
+    } else {
+      a.x = F::unpack(w);
+      a.y = F::unpack(w + PW);
+    }
     if (e_cur & 0x80000000u) a = C::neg_affine(a);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
     if (j + 1 < end) {
