@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU box: PMC passes over the 2^22 bench (2 proofs), one counter group per run
-# (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass; <= 8 SQ, 4 TCC counters).
+# (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass; <= 8 SQ, 4 TCC, 2 GRBM counters).
+# GRBM_GUI_ACTIVE / 8 XCDs / kernel wall time = the clock the chip held during the kernel ('DVFS give-back').
 # Output: gpurun_out/pmc/<pass>/run_counter_collection.csv
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/pmc
@@ -12,4 +13,5 @@ run() {  # name counters...
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU && \
-run tcc TCC_HIT_sum TCC_MISS_sum
+run tcc TCC_HIT_sum TCC_MISS_sum && \
+run grbm GRBM_GUI_ACTIVE GRBM_COUNT
