@@ -557,6 +557,14 @@ bh_status plan_shard(bh_ctx* ctx, const bh_params* params_c, const bh_witness* w
                w->b_in_total);                                                                         // b_g2_aux
   jobs[1] = mk(false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5, &w->b_aux_density, &w->b_aux_prefix,
                w->b_in_total);                                                                         // b_g1_aux
+  // BH_G1_FIRST=1 (A/B): b_g1_aux sorted and accumulated first, b_g2_aux copying its sort second --
+  // a G2 accumulation wave takes a SIMD's whole register file, so nothing (e.g. a distributed H's
+  // passes) can share its SIMDs, while a G1 accumulation (2 x 180 VGPRs) leaves room for one
+  static const bool g1_first = [] {
+    const char* e = getenv("BH_G1_FIRST");
+    return e && e[0] == '1';
+  }();
+  if (g1_first) std::swap(jobs[0], jobs[1]);
   jobs[2] = mk(false, &params->l, aux, na, nullptr, na, 1, nullptr, nullptr, 0);                       // l
   jobs[3] = mk(false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3, &w->a_aux_density, &w->a_aux_prefix,
                ni);                                                                                    // a_aux
