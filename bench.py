@@ -35,7 +35,8 @@ G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip 
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
 PMC_FILE = "r03_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench
-SOLO_WAVE_INSTR_RATE = 515.0   # G wave-instr/s: the G1 accumulation alone (6.3 G madd/s x 5234 lane-instr / 64)
+SOLO_WAVE_INSTR_RATE = 510.0   # G wave-instr/s: the G1 accumulation alone (6.38 G madd/s x 5116 lane-instr / 64;
+                               # profiles/r03_ab_accumulate_variants.txt serial run, r03_pmc_2p22.json)
 
 
 def parse():
@@ -373,7 +374,7 @@ def main():
                           "peak": SOLO_WAVE_INSTR_RATE, "unit": "G VALU wave-instructions/s",
                           "frac": round(rate / SOLO_WAVE_INSTR_RATE, 4),
                           "source": f"profiles/{PMC_FILE} (SQ_INSTS_VALU, every dispatch) / this run's ms_per_step",
-                          "peak_source": "k_accumulate_pf<G1> alone (BH_PROVER_SERIAL=1): 6.3 G madd/s x 5234 / 64"}
+                          "peak_source": "k_accumulate_pf<G1> alone (BH_PROVER_SERIAL=1): 6.38 G madd/s x 5116 / 64"}
     c5 = c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier) if args.c5 else None
     if rank != 0:
         comm.close()
