@@ -116,6 +116,38 @@ def test_msm_identity_base_semantics(ctx, golden):
         assert got == want
 
 
+@pytest.mark.parametrize("g2", [False, True])
+def test_msm_exceptional_additions_in_one_bucket(ctx, g2):
+    """Equal and opposite bases under equal exponents land next to each other in one bucket per
+    window, so the accumulation meets acc == base (a doubling) and acc == -base (the identity), and
+    the reductions add equal partial sums: the cases curve.cuh folds into the addition's own
+    instruction stream (G1 madd, both groups' full addition).  Compared with the oracle's multiexp
+    (multiexp.rs:159-281)."""
+    bh = _bh()
+    from oracle import bellman as bm
+    from oracle import bls12_381 as bls
+    E = bm.BLS12_381
+    G = E.G2 if g2 else E.G1
+    gen = bls.G2.generator() if g2 else bls.G1.generator()
+    enc = bls.g2_to_uncompressed if g2 else bls.g1_to_uncompressed
+    aff = lambda k: G.to_affine(G.mul(gen, k % R))
+    P, N, Q = aff(11), aff(R - 11), aff(29)
+    rng = random.Random(21)
+    others = [aff(rng.randrange(1, R)) for _ in range(8)]
+    pts = [P] * 24 + [N] * 24 + [Q] * 16 + others
+    bases = bh.Bases(ctx, bh.BH_G2 if g2 else bh.BH_G1, b"".join(enc(p) for p in pts))
+    e1, e2 = rng.randrange(R), rng.randrange(R)
+    cases = [
+        [e1] * 48 + [e2] * 16 + [rng.randrange(R) for _ in range(8)],     # 24P - 24P + 16 e2 Q + ...
+        [e1] * 24 + [e2] * 24 + [e1] * 16 + [rng.randrange(R) for _ in range(8)],
+        [e1] * 48 + [0] * 24,                                             # the exact identity
+        [1] * 24 + [R - 1] * 24 + [2] * 16 + [0] * 8,                      # small digits, one bucket
+    ]
+    for exps in cases:
+        want = enc(G.to_affine(bm.multiexp(E, G, pts, 0, None, exps)))
+        assert bh.multiexp(ctx, bases, 0, None, exps) == want
+
+
 def test_msm_density_mismatch(ctx, golden):
     bh = _bh()
     bases = _bases(ctx, bh.BH_G1, golden["msm_g1"]["bases"][:10])
