@@ -358,6 +358,16 @@ def main():
             "mad_u64_tps": round(madd_rate * MADS_PER_G1_MADD / 1e3, 2) if madd_rate else None,
             "mad_u64_frac": round(madd_rate * MADS_PER_G1_MADD / 1e3 / MAD_U64_PEAK_TPS, 4) if madd_rate else None,
             "mad_u64_peak_tps": MAD_U64_PEAK_TPS, "mad_u64_peak_source": "tools/microbench/madbench.hip"}
+    # the clock the chip holds under this kernel (GRBM_GUI_ACTIVE / 8 XCDs / wall time, from the
+    # committed PMC passes; 2.4 GHz peak): the VALU peaks above are per-clock rates at whatever
+    # clock the microbenchmark ran ('DVFS')
+    cpath = os.path.join(ROOT, "profiles", PMC_FILE)
+    if os.path.exists(cpath):
+        with open(cpath) as f:
+            g1pmc = json.load(f).get("k_accumulate_pf<CurveOps<FpOps", {})
+        if "held_clock_ghz" in g1pmc:
+            valu["held_clock_ghz"] = g1pmc["held_clock_ghz"]
+            valu["held_clock_source"] = f"profiles/{PMC_FILE} (GRBM_GUI_ACTIVE, counter passes)"
     # whole-proof VALU issue: the PMC pass's VALU wave-instructions per proof (every kernel)
     # against the rate the G1 accumulation issues at alone
     proof_valu = None
