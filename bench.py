@@ -32,6 +32,7 @@ G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point
 G2_PAIR_BYTES = 224
 TRAFFIC_FILE = "r03_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
 G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X (profiles/r01_curvebench.txt)
+G1_MADD_PEAK_CLOCK_GHZ = 2.27  # the clock curvebench's G1 (2 waves) kernel held (profiles/r03_curvebench_clock.txt)
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
 PMC_FILE = "r03_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench
@@ -368,6 +369,12 @@ def main():
         if "held_clock_ghz" in g1pmc:
             valu["held_clock_ghz"] = g1pmc["held_clock_ghz"]
             valu["held_clock_source"] = f"profiles/{PMC_FILE} (GRBM_GUI_ACTIVE, counter passes)"
+            # the microbenchmark peak was taken at its own held clock: scaled to this kernel's
+            scaled = G1_MADD_PEAK * g1pmc["held_clock_ghz"] / G1_MADD_PEAK_CLOCK_GHZ
+            valu["peak_clock_scaled"] = round(scaled, 3)
+            valu["frac_clock_scaled"] = round(madd_rate / scaled, 4) if madd_rate else None
+            valu["peak_clock_source"] = ("curvebench at %.2f GHz (profiles/r03_curvebench_clock.txt)"
+                                         % G1_MADD_PEAK_CLOCK_GHZ)
     # whole-proof VALU issue: the PMC pass's VALU wave-instructions per proof (every kernel)
     # against the rate the G1 accumulation issues at alone
     proof_valu = None
