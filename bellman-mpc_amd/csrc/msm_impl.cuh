@@ -458,8 +458,10 @@ void fit_segments(MsmShape& sh, size_t n) {
   }();
   // BH_ACC_FILL: fraction of the resident capacity the accumulation occupies per round
   // (the rest stays free for the side streams' short kernels)
+  // (BH_ACC_FILL_G1 / BH_ACC_FILL_G2: the same for one group only)
   static const double fill = [] {
-    const char* e = getenv("BH_ACC_FILL");
+    const char* e = getenv(std::is_same<C, G1Ops>::value ? "BH_ACC_FILL_G1" : "BH_ACC_FILL_G2");
+    if (!e) e = getenv("BH_ACC_FILL");
     const double f = e ? atof(e) : 1.0;
     return (f > 0.0 && f <= 1.0) ? f : 1.0;
   }();
