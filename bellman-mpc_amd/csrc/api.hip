@@ -723,6 +723,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   BH_TRY_HIP(hipSetDevice(device));
   bh_ctx* c = new bh_ctx();
   c->device = device;
+  c->attach_affine();
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -816,6 +817,8 @@ __attribute__((visibility("hidden"))) bh_status ctx_create_lane(bh_ctx* primary,
   for (int q = 0; q < bh_ctx::TAIL_STREAMS; q++) c->tstream[q] = primary->tstream[q];
   c->tables = primary->tables;
   c->window_override = primary->window_override;
+  c->aff1 = primary->aff1;
+  c->attach_affine();
   bool ok = true;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (auto& e : c->jev) ok = ok && hipEventCreate(&e) == hipSuccess;
@@ -1094,6 +1097,7 @@ static bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar
   static std::atomic<uint64_t> next_id{1};
   auto buf = std::make_shared<bh_scalar_buf>();
   buf->device = ctx->device;
+  buf->owner = ctx;
   buf->id = next_id.fetch_add(1);
   BH_TRY_HIP(buf->d.alloc(std::max<size_t>(n, 1) * 32));
   BH_TRY_HIP(hipEventCreateWithFlags(&buf->ready, hipEventDisableTiming));

@@ -140,7 +140,8 @@ struct bh_params {
   // gathered into share order so that a shard-sized window table covers them; key (N, rank, L)
   std::map<std::tuple<int, int, int>, std::unique_ptr<bh_srs>> h_shares;
   // host copies of the leading bases of a, b_g1, b_g2 (the public inputs' bases), read back from
-  // the device on first use (under mu, exclusively) for the host input multiexps
+  // the device on first use for the host input multiexps: under head_mu, only ever grown, and
+  // each proof copies the points it needs out while holding it (prover.hip host_input_msms)
   std::mutex head_mu;
   std::vector<bh::AffinePt<bh::Fp>> h_a_head, h_b1_head;
   std::vector<bh::AffinePt<bh::Fp2>> h_b2_head;
@@ -158,6 +159,9 @@ constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use pla
 struct bh_scalar_buf {
   bh::DevBuf d;
   uint64_t id = 0;  // unique per vector (jobs' sort sharing is keyed on it, not on d's address)
+  // the context whose producer thread (if any) makes it: only that context may park deferred
+  // enqueues on it (its teardown waits for its producers, which run them)
+  const bh_ctx* owner = nullptr;
   hipEvent_t ready = nullptr;
   int device = 0;
   std::mutex mu;
@@ -228,6 +232,13 @@ struct bh_ctx {
   // tails of different multiexps never share buffers (about 1 GB each at 2^22 points)
   bh::MsmWorkspace<G1Ops> pw1[6];
   bh::MsmWorkspace<G2Ops> pw2[2];
+  // batch-affine level buffers of the G1 accumulations on `stream` (msm.h; shared with the lanes
+  // that borrow this context's streams: the main stream serialises their use)
+  std::shared_ptr<bh::AffineBufs> aff1 = std::make_shared<bh::AffineBufs>();
+  void attach_affine() {
+    for (auto& w : pw1) w.aff = aff1.get();
+    g1ws.aff = aff1.get();
+  }
   XYZZ<G1F>* host_out1 = nullptr;     // pinned, 8 jobs x 128 windows (c >= 2)
   XYZZ<Fp2Ops>* host_out2 = nullptr;  // pinned, 2 jobs x 128 windows
   hipEvent_t jev[48] = {};

@@ -110,6 +110,7 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
                       size_t set, const uint64_t* density_words, const uint32_t* d_scalars, bool tables,
                       const JobStreams& st) {
   const uint32_t* pts = bases->pts.as<uint32_t>();
+  ws.aff = ctx->aff1.get();  // (the accumulation runs on ctx->stream, as the prover's)
   bool tab = false;
   if (tables && set >= TABLE_MIN_USED) {
     std::lock_guard<std::mutex> lk(bases->win_mu);
@@ -250,11 +251,13 @@ bh_status enqueue_job(bh_ctx* ctx, bh_job* job, const bh_srs* bases, size_t base
     return e;
   };
   const size_t set = density_set(density_words, n);
+  // window tables as the prover uses them: not under a forced window size (bh_ctx_set_window)
+  const bool tables = ctx->tables && !job->window_override;
   bh_status s = bases->group == BH_G1
                     ? enqueue_msm<G1Ops>(ctx, job, sl->ws1, bases, base_offset, n, set, density_words, d_scalars,
-                                         ctx->tables, js)
+                                         tables, js)
                     : enqueue_msm<G2Ops>(ctx, job, sl->ws2, bases, base_offset, n, set, density_words, d_scalars,
-                                         ctx->tables, js);
+                                         tables, js);
   if (s) return fail(s);
   return BH_OK;
 }
@@ -402,6 +405,15 @@ bh_status bh_multiexp_submit_scalars(bh_ctx* ctx, const bh_srs* bases, size_t ba
   {
     std::unique_lock<std::mutex> lk(buf->mu);
     if (!buf->enqueued) {
+      // the producer thread will run this enqueue on ctx: only the producing context's own
+      // teardown waits for that thread, so a vector still being produced by another context is
+      // refused (a submit after its bh_scalars_sync is fine from any context of the device)
+      if (buf->owner != ctx) {
+        lk.unlock();
+        give_slot(*jp->reg, jp->slot);
+        jp->slot = nullptr;
+        return BH_ERR_INVALID_ARGUMENT;
+      }
       std::vector<uint64_t> dens;  // the caller's density words are read before submit returns
       if (density_words) dens.assign(density_words, density_words + (n + 63) / 64);
       buf->deferred.push_back([work, dens = std::move(dens)](bh_status up) {

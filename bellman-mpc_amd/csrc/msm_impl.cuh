@@ -127,11 +127,14 @@ __device__ __forceinline__ uint32_t block_span(const uint32_t* words, uint32_t g
 // segments costs 4 + 2 serial additions instead of 15.  The tails are VALU-bound chains
 // on a small fraction of the SIMDs: serial depth is their latency.
 // span_words != null (device-decided): the whole grid returns when the longest span is at most
-// fold_span (k_reduce_blocks folds those), and otherwise folds every span, however long.
+// fold_span (k_reduce_blocks folds those), and otherwise folds every bucket spanning at most
+// seq_max segments; longer ones are k_cont_long's (a serial chain over thousands of partials
+// would be the tail's latency: a witness full of ones puts most entries in one bucket).
 template <class C, int Q>
 __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
                                                   uint32_t nbr, uint32_t S, typename C::P* conts,
-                                                  const uint32_t* span_words, uint32_t span_g, uint32_t fold_span) {
+                                                  const uint32_t* span_words, uint32_t span_g, uint32_t fold_span,
+                                                  uint32_t seq_max) {
   extern __shared__ uint4 lds_raw[];
   typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
   if (span_words && block_span(span_words, span_g) <= fold_span) return;
@@ -144,6 +147,7 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32
       const uint32_t off = offsets[b];
       s_first = off / S;
       ncont = (off + cnt - 1) / S - s_first;  // partials conts[s_first+1 .. s_first+ncont]
+      if (span_words && ncont > seq_max) ncont = 0;  // k_cont_long's
     }
   }
   typename C::P acc = C::identity();
@@ -159,6 +163,67 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32
     __syncthreads();
   }
   if (q == 0 && ncont >= 2) store_point<C>(&conts[s_first + 1], acc);
+}
+
+// Device-decided tails, buckets spanning more than seq_max segments (rare: a bucket holding a
+// large share of the entries): one workgroup per such bucket, its threads summing strided
+// partials, then an LDS tree, into conts[s_first+1].  A grid-stride pass over the buckets finds
+// them; the whole grid returns at once when the longest span is at most seq_max.
+template <class C>
+__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_long(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
+                                                   uint32_t nbr, uint32_t S, typename C::P* conts,
+                                                   const uint32_t* span_words, uint32_t span_g, uint32_t seq_max) {
+  extern __shared__ uint4 lds_raw[];
+  typename C::P* lds = reinterpret_cast<typename C::P*>(lds_raw);
+  __shared__ uint32_t list[256];
+  __shared__ uint32_t nlist;
+  if (block_span(span_words, span_g) <= seq_max) return;
+  const uint32_t tid = threadIdx.x, BT = blockDim.x;
+  for (uint32_t base = blockIdx.x * BT; base < nbr; base += gridDim.x * BT) {
+    if (tid == 0) nlist = 0;
+    __syncthreads();
+    if (base + tid < nbr) {
+      const uint32_t b = b0 + base + tid, cnt = counts[b];
+      if (cnt) {
+        const uint32_t off = offsets[b];
+        if ((off + cnt - 1) / S - off / S > seq_max) list[atomicAdd(&nlist, 1u)] = b;
+      }
+    }
+    __syncthreads();
+    const uint32_t nl = nlist;
+    for (uint32_t li = 0; li < nl; li++) {
+      const uint32_t b = list[li], off = offsets[b];
+      const uint32_t s_first = off / S, ncont = (off + counts[b] - 1) / S - s_first;
+      // ceil(ncont / BT) strided steps, then log2(BT) tree steps: one addition call site (a G2
+      // addition inlined twice doubles the unit's compile time)
+      const uint32_t nit = (ncont + BT - 1) / BT;
+      uint32_t lg = 0;
+      while ((1u << lg) < BT) lg++;
+      typename C::P acc = C::identity();
+      for (uint32_t st = 0; st < nit + lg; st++) {
+        typename C::P x;
+        bool act;
+        if (st < nit) {
+          const uint32_t i = st * BT + tid;
+          act = i < ncont;
+          if (act) x = load_point<C>(&conts[s_first + 1 + i]);
+        } else {
+          if (st == nit) store_point<C>(&lds[tid], acc);
+          __syncthreads();
+          const uint32_t h = BT >> (st - nit + 1);
+          act = tid < h;
+          if (act) x = load_point<C>(&lds[tid + h]);
+        }
+        if (act) acc = C::add(acc, x);
+        if (st >= nit) {
+          __syncthreads();
+          if (act) store_point<C>(&lds[tid], acc);
+        }
+      }
+      if (tid == 0) store_point<C>(&conts[s_first + 1], acc);
+      __syncthreads();
+    }
+  }
 }
 
 // ---- Bucket reduction: window total  sum_{b < NB} (b+1) * B_b  (bucket b holds digit b+1;
@@ -367,9 +432,10 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   constexpr bool G1 = std::is_same<C, G1Ops>::value;
   constexpr int NW = sizeof(typename F::T) / 4;    // raw limb words per coordinate (G1: 14)
   constexpr int NQ = G1 ? NW / 2 : 2 * PW / 4;     // 16-byte pieces per base (G1: up to 7)
-  // G1 window-table records hold raw limbs (G1_TABLE_REC, 7 pieces, no unpacking); plain
-  // vectors are packed (6 pieces)
-  const bool limbs = G1 && rec == G1_TABLE_REC;
+  // G1 window-table records hold raw limbs (G1_TABLE_REC, 7 pieces, no unpacking), and so do the
+  // batch-affine levels' records (G1_AFF_REC: read in order, entries == null; a record of the
+  // point at infinity, AFF_IDENT, is skipped); plain vectors are packed (6 pieces)
+  const bool limbs = G1 && (rec == G1_TABLE_REC || rec == G1_AFF_REC);
   const int nq = limbs ? NQ : 2 * PW / 4;
   __shared__ uint4 pre[4][NQ][64];
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
@@ -387,9 +453,10 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 4 * q),
                                          (__attribute__((address_space(3))) void*)&pre[wv][q][0], 16, 0, 0);
   };
-  uint32_t e_cur = entries[start];
+  auto entry = [&](uint32_t j) { return entries ? entries[j] : j; };
+  uint32_t e_cur = entry(start);
   issue(e_cur);
-  uint32_t e_next = (start + 1 < end) ? entries[start + 1] : 0u;
+  uint32_t e_next = (start + 1 < end) ? entry(start + 1) : 0u;
   uint32_t b = find_bucket(offsets, nbt, start);
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
@@ -426,13 +493,14 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
       a.y = F::unpack(w + PW);
     }
     if (e_cur & 0x80000000u) a = C::neg_affine(a);
+    const bool skip = limbs && (w[NW - 1] & AFF_IDENT);  // (a level record of the point at infinity)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
     if (j + 1 < end) {
       issue(e_next);
       e_cur = e_next;
-      e_next = (j + 2 < end) ? entries[j + 2] : 0u;
+      e_next = (j + 2 < end) ? entry(j + 2) : 0u;
     }
-    acc = C::madd(acc, a);
+    if (!skip) acc = C::madd(acc, a);
   }
   if (started_here) store_point<C>(&bucket_sums[b], acc);
   else store_point<C>(&conts[seg], acc);
@@ -442,7 +510,13 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
 // resident workgroups (occupancy from the compiled kernel, CUs from the device): a
 // partial last round would leave most of the chip idle for its whole duration.
 template <class C>
+void fit_segments_E(MsmShape& sh, size_t E);
+template <class C>
 void fit_segments(MsmShape& sh, size_t n) {
+  fit_segments_E<C>(sh, n * (size_t)sh.W);
+}
+template <class C>
+void fit_segments_E(MsmShape& sh, size_t E) {
   static const size_t conc = [] {
     int dev = 0, cus = 256, blocks = 1;
     (void)hipGetDevice(&dev);
@@ -472,10 +546,27 @@ void fit_segments(MsmShape& sh, size_t n) {
     const long v = e ? atol(e) : 8;
     return (size_t)(v >= 1 ? v : 8);
   }();
-  const size_t E = n * (size_t)sh.W;
   const size_t slots = std::max<size_t>((size_t)(rounds * conc * fill) / 256 * 256, 256);
   size_t S = (E + slots - 1) / slots;
   sh.S = (int)std::min<size_t>(std::max<size_t>(S, min_s), (size_t)1 << 16);
+}
+
+// The batch-affine levels of this workspace's multiexp (msm.h): G1 window-table shapes on a
+// workspace with the context's level buffers; S = the XYZZ segment length over the last level.
+template <class C>
+AffinePlan affine_plan_for(const MsmWorkspace<C>& ws, size_t n, const MsmShape& sh) {
+  AffinePlan pl;
+  if constexpr (std::is_same<C, G1Ops>::value) {
+    if (ws.aff && sh.rec == (int)G1_TABLE_REC && n > 0) {
+      pl = affine_plan_g1(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves);
+      if (pl.levels) {
+        MsmShape s2 = sh;
+        fit_segments_E<C>(s2, pl.Eb[pl.levels]);
+        pl.S = s2.S;
+      }
+    }
+  }
+  return pl;
 }
 
 template <class C>
@@ -594,6 +685,11 @@ void MsmWorkspace<C>::release() {
   if (seg_sum) hipFree(seg_sum);
   if (window_sums) hipFree(window_sums);
   if (host_window_sums) hipHostFree(host_window_sums);
+  for (uint32_t** p : {&aoff, &acnt, &ascan, &aspan}) {
+    if (*p) hipFree(*p);
+    *p = nullptr;
+  }
+  cap_anbt = 0;
   entries = counts = offsets = cursor = scan_scratch = nullptr;
   bucket_sums = conts = seg_weighted = seg_sum = window_sums = nullptr;
   host_window_sums = nullptr;
@@ -622,6 +718,24 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
+    if constexpr (std::is_same<C, G1Ops>::value) {
+      const AffinePlan pl = affine_plan_for<C>(ws, n, sh);
+      if (pl.levels) {  // batch-affine levels, then the XYZZ accumulation over the last level's records
+        // (the level buffers are the context's: held from their sizing to the last launch reading them)
+        std::lock_guard<std::mutex> lk(ws.aff->mu);
+        const uint32_t* fin = nullptr;
+        hipError_t e = affine_levels_g1(ws, st, d_bases, rec, pl, nbt, &fin);
+        if (e != hipSuccess) return e;
+        const size_t fsegs = (pl.Eb[pl.levels] + pl.S - 1) / pl.S;
+        if ((e = ws.grow(0, 0, fsegs + 1, 0)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(fsegs, 256)), dim3(256), 0, st,
+                           (const uint32_t*)nullptr, ws.aoff + (size_t)(pl.levels - 1) * (nbt + 1), (uint32_t)nbt,
+                           fin, G1_AFF_REC, (uint32_t)pl.S, 0u, (uint32_t)nbt, ws.bucket_sums, ws.conts,
+                           ws.cont_bucket);
+        if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
+        return hipGetLastError();
+      }
+    }
     const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
     hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
                        ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, 0u, cut, ws.bucket_sums, ws.conts,
@@ -650,28 +764,52 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 // fix-up, then the two-level summation by parts into out[] (Wb totals, or 3 points when split).
 struct SpanSrc {  // device-decided tails: k_max_span's words (null: the host decided)
   const uint32_t* words = nullptr;
-  uint32_t g = 0, fold_span = 0;
+  uint32_t g = 0, fold_span = 0, seq_max = 0;
 };
 
+// The sorted view the accumulation left for the reduction: the sort's counts/offsets and the
+// shape's S, or the last batch-affine level's (counts ceil(c / 2^levels), segments of plan.S).
+struct AccView {
+  const uint32_t *counts, *offsets;
+  uint32_t S;
+  size_t E;  // upper bound of the accumulated records
+  const uint32_t* span_words;  // the last level's max-span words (null: the sort's)
+};
 template <class C>
-static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh, size_t segs, size_t span,
-                         bool fold, bool seq, uint32_t b0, uint32_t nbr, uint32_t L, uint32_t y_off,
+AccView acc_view(const MsmWorkspace<C>& ws, size_t n, const MsmShape& sh) {
+  const AffinePlan pl = affine_plan_for<C>(ws, n, sh);
+  if (pl.levels) {
+    const size_t nbt = (size_t)sh.Wb * sh.NB;
+    return AccView{ws.acnt, ws.aoff + (size_t)(pl.levels - 1) * (nbt + 1), (uint32_t)pl.S, pl.Eb[pl.levels], ws.aspan};
+  }
+  return AccView{ws.counts, ws.offsets, (uint32_t)sh.S, n * (size_t)sh.W, nullptr};
+}
+
+template <class C>
+static void reduce_range(MsmWorkspace<C>& ws, const AccView& v, hipStream_t st, const MsmShape& sh, size_t segs,
+                         size_t span, bool fold, bool seq, uint32_t b0, uint32_t nbr, uint32_t L, uint32_t y_off,
                          typename C::P* out, const SpanSrc& dev = SpanSrc()) {
   constexpr bool G2 = sizeof(typename C::P) > 256;
   const size_t nb_all = (size_t)sh.Wb * nbr;
+  const size_t nbt = (size_t)sh.Wb * sh.NB;
   if (dev.words || (!fold && seq)) {
     constexpr int Q = 4;
     constexpr uint32_t B = G2 ? 128 : 256;  // LDS: B points
     if (dev.words || span >= 2)
       hipLaunchKernelGGL((k_cont_seq<C, Q>), dim3(msm_blocks_for(nb_all * Q, B)), dim3(B), B * sizeof(typename C::P),
-                         st, ws.counts, ws.offsets, b0, (uint32_t)nb_all, (uint32_t)sh.S, ws.conts, dev.words, dev.g,
-                         dev.fold_span);
+                         st, v.counts, v.offsets, b0, (uint32_t)nb_all, v.S, ws.conts, dev.words, dev.g,
+                         dev.fold_span, dev.seq_max);
+    // device-decided spans beyond seq_max: one workgroup per such bucket (returns at once when
+    // there is none)
+    if (dev.words)
+      hipLaunchKernelGGL((k_cont_long<C>), dim3(std::min<unsigned>(msm_blocks_for(nb_all, B), 256u)), dim3(B),
+                         B * sizeof(typename C::P), st, v.counts, v.offsets, b0, (uint32_t)nb_all, v.S, ws.conts,
+                         dev.words, dev.g, dev.seq_max);
   } else if (!fold) {
-    const size_t nbt = (size_t)sh.Wb * sh.NB;
     for (size_t stride = 1; stride < span; stride *= 4)
       hipLaunchKernelGGL((k_cont_treeF<C, 4>), dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.cont_bucket,
-                         ws.counts, ws.offsets, (uint32_t)nbt, (uint32_t)sh.S, (uint32_t)stride, b0,
-                         (uint32_t)(b0 + nb_all), ws.conts);
+                         v.counts, v.offsets, (uint32_t)nbt, v.S, (uint32_t)stride, b0, (uint32_t)(b0 + nb_all),
+                         ws.conts);
   }
   // two-level summation by parts (k_reduce_blocks, k_reduce_window): Y/S per level-1 block
   // in seg_weighted / seg_sum (from y_off), the totals in out
@@ -682,9 +820,8 @@ static void reduce_range(MsmWorkspace<C>& ws, hipStream_t st, const MsmShape& sh
   const uint32_t Lb = nblk / BT2;
   const int split = sh.Wb == 1 ? 1 : 0;
   hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
-                     ws.counts, ws.offsets, ws.bucket_sums, ws.conts, (uint32_t)sh.S, b0, (uint32_t)sh.NB, L,
-                     reduce_lg2(L), nblk, fold ? 1 : 0, ws.seg_weighted + y_off, ws.seg_sum + y_off, dev.words, dev.g,
-                     dev.fold_span);
+                     v.counts, v.offsets, ws.bucket_sums, ws.conts, v.S, b0, (uint32_t)sh.NB, L, reduce_lg2(L), nblk,
+                     fold ? 1 : 0, ws.seg_weighted + y_off, ws.seg_sum + y_off, dev.words, dev.g, dev.fold_span);
   hipLaunchKernelGGL(k_reduce_window<C>, dim3((unsigned)sh.Wb), dim3(BT2), 2 * BT2 * sizeof(typename C::P), st,
                      ws.seg_weighted + y_off, ws.seg_sum + y_off, nblk, Lb, reduce_lg2(Lb),
                      reduce_lg2(L) + reduce_lg2(BT), split, out);
@@ -702,7 +839,12 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
     const char* e = getenv("BH_FOLD_SPAN");
     return e ? (size_t)atol(e) : (size_t)8;
   }();
-  const size_t segs = (n * (size_t)sh.W + sh.S - 1) / sh.S;
+  const AccView v = acc_view<C>(ws, n, sh);
+  if (v.span_words) {  // batch-affine levels: the last level's spans, read on the device
+    max_span = -1;
+    d_span_words = v.span_words;
+  }
+  const size_t segs = (v.E + v.S - 1) / v.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
   const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;
   const bool seq = max_span >= 0 && span <= cont_seq_max();
@@ -711,17 +853,18 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
     dev.words = d_span_words;
     dev.g = max_span_blocks((size_t)sh.Wb * sh.NB);
     dev.fold_span = (uint32_t)REDUCE_FOLD_SPAN;
+    dev.seq_max = (uint32_t)cont_seq_max();
   }
   if (sh.halves) {
     const uint32_t nbh = (uint32_t)sh.NB / 2;
-    reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums, dev);
+    reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums, dev);
     if (acc_done) hipStreamWaitEvent(st, acc_done, 0);
     const uint32_t y_off = nbh / sh.L / reduce_threads_for(nbh, (uint32_t)sh.L, sizeof(typename C::P) > 256);
-    reduce_range<C>(ws, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3, dev);
+    reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3, dev);
     hipMemcpyAsync(host_out, ws.window_sums, 6 * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
     return hipGetLastError();
   }
-  reduce_range<C>(ws, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums, dev);
+  reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums, dev);
   hipMemcpyAsync(host_out, ws.window_sums, (sh.Wb == 1 ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost,
                  st);
   return hipGetLastError();

@@ -479,23 +479,33 @@ bh_status host_input_msms(int device, bh_params* p, const bh_witness* w, size_t 
   for (size_t i = 0; i < lo; i++) nb += bit(i);
   size_t nb_hi = nb;
   for (size_t i = lo; i < hi; i++) nb_hi += bit(i);
+  // The cache only grows (a rank never shrinks what another one read), and this rank's points are
+  // copied out under the lock: N rank threads share one bh_params (run_ranks), with different
+  // [lo, hi) ranges, and a concurrent refill may reallocate the vectors.
+  std::vector<AffinePt<Fp>> a_pts, b1_pts;
+  std::vector<AffinePt<bh::Fp2>> b2_pts;
   {
     std::lock_guard<std::mutex> lk(p->head_mu);
-    if (p->h_a_head.size() < hi || p->h_b1_head.size() < nb_hi) {
+    if (p->h_a_head.size() < hi || p->h_b1_head.size() < nb_hi || p->h_b2_head.size() < nb_hi) {
       if (hipSetDevice(device) != hipSuccess) return BH_ERR_HIP;
+      const size_t na = std::max(hi, p->h_a_head.size());
+      const size_t nb2 = std::max(nb_hi, std::max(p->h_b1_head.size(), p->h_b2_head.size()));
       bh_status s;
-      if ((s = read_head<false>(p->a, hi, &p->h_a_head))) return s;
-      if ((s = read_head<false>(p->b_g1, nb_hi, &p->h_b1_head))) return s;
-      if ((s = read_head<true>(p->b_g2, nb_hi, &p->h_b2_head))) return s;
+      if ((s = read_head<false>(p->a, na, &p->h_a_head))) return s;
+      if ((s = read_head<false>(p->b_g1, nb2, &p->h_b1_head))) return s;
+      if ((s = read_head<true>(p->b_g2, nb2, &p->h_b2_head))) return s;
     }
+    a_pts.assign(p->h_a_head.begin() + lo, p->h_a_head.begin() + hi);
+    b1_pts.assign(p->h_b1_head.begin() + nb, p->h_b1_head.begin() + nb_hi);
+    b2_pts.assign(p->h_b2_head.begin() + nb, p->h_b2_head.begin() + nb_hi);
   }
-  for (size_t i = lo; i < hi; i++) {
+  for (size_t i = lo, j = 0; i < hi; i++) {
     const uint64_t* k = &w->h_inputs[4 * i];
-    *r_a = jac_add(*r_a, jac_mul(jac_from_affine(p->h_a_head[i]), k, 4));
+    *r_a = jac_add(*r_a, jac_mul(jac_from_affine(a_pts[i - lo]), k, 4));
     if (bit(i)) {
-      *r_b1 = jac_add(*r_b1, jac_mul(jac_from_affine(p->h_b1_head[nb]), k, 4));
-      *r_b2 = jac_add(*r_b2, jac_mul(jac_from_affine(p->h_b2_head[nb]), k, 4));
-      nb++;
+      *r_b1 = jac_add(*r_b1, jac_mul(jac_from_affine(b1_pts[j]), k, 4));
+      *r_b2 = jac_add(*r_b2, jac_mul(jac_from_affine(b2_pts[j]), k, 4));
+      j++;
     }
   }
   return BH_OK;

@@ -217,8 +217,10 @@ def main():
     # the hardware-queue setting the library will raise (include/bellman_hip.h), recorded as found
     hwq_env = os.environ.get("GPU_MAX_HW_QUEUES")
     hwq_keep = os.environ.get("BH_KEEP_HW_QUEUES") == "1"
-    hw_queues = {"env": hwq_env, "effective": hwq_env if hwq_keep or (hwq_env and int(hwq_env) >= 16) else "16",
-                 "raised_by_library": not hwq_keep and not (hwq_env and int(hwq_env) >= 16)}
+    # (the library reads it with atoi: an unparseable value counts as 0 and is raised too)
+    hwq_ok = bool(hwq_env) and hwq_env.strip().isdigit() and int(hwq_env) >= 16
+    hw_queues = {"env": hwq_env, "effective": hwq_env if hwq_keep or hwq_ok else "16",
+                 "raised_by_library": not hwq_keep and not hwq_ok}
     if spawn:
         # plain `python bench.py --gpus N`: start the N rank processes (one per GPU, LOCAL_RANK =
         # device) before this parent touches HIP, and exit with the first failing rank's code
