@@ -81,6 +81,8 @@ struct MsmTiming {
 // Record of a level: x then y as 14 + 14 raw 29-bit limbs (112 B); the point at infinity (a
 // P + (-P) pair) has AFF_IDENT set in x's top limb word.
 constexpr uint32_t G1_AFF_REC = 28;
+constexpr uint32_t G2_AFF_REC = 56;   // (x.c0, x.c1, y.c0, y.c1: 4 x 14 raw limbs, 224 B)
+constexpr uint32_t G2_TABLE_REC = 64; // G2 window-table record: packed x, y (48 words) in a 256-B line
 constexpr uint32_t AFF_IDENT = 0x80000000u;
 constexpr int AFF_LMAX = 8;
 
@@ -108,9 +110,10 @@ struct AffinePlan {
   size_t Eb[AFF_LMAX + 1] = {};   // upper bound of the records after each level (Eb[0]: entries)
   int S = 0;                      // segment length of the XYZZ accumulation over the last level
 };
-// (nbt buckets, Emax = n*W entries at most); levels = 0 unless the group is G1, the context has
-// AffineBufs and the level's pairs fill at least BH_AFF_KMIN (16) per thread
+// (nbt buckets, Emax = n*W entries at most); levels = 0 unless the context has AffineBufs, the
+// bases are a window table and the level's pairs fill at least BH_AFF_KMIN (16) per thread
 AffinePlan affine_plan_g1(size_t Emax, size_t nbt, int halves);
+AffinePlan affine_plan_g2(size_t Emax, size_t nbt, int halves);
 
 template <class C>
 struct MsmWorkspace {
@@ -207,7 +210,25 @@ size_t derive_scratch_words(size_t Emax);
 // G1_AFF_REC words each) for the XYZZ accumulation, or null when plan.levels == 0
 hipError_t affine_levels_g1(MsmWorkspace<G1Ops>& ws, hipStream_t st, const uint32_t* d_bases, uint32_t rec,
                             const AffinePlan& plan, size_t nbt, const uint32_t** final_pts);
-hipError_t affine_reserve_g1(MsmWorkspace<G1Ops>& ws, size_t nbt);
+hipError_t affine_levels_g2(MsmWorkspace<G2Ops>& ws, hipStream_t st, const uint32_t* d_bases, uint32_t rec,
+                            const AffinePlan& plan, size_t nbt, const uint32_t** final_pts);
+// per-workspace level geometry arrays (aoff, acnt, ascan, aspan) for nbt buckets
+template <class C>
+hipError_t affine_reserve(MsmWorkspace<C>& ws, size_t nbt) {
+  if (nbt <= ws.cap_anbt && ws.aoff) return hipSuccess;
+  for (uint32_t** p : {&ws.aoff, &ws.acnt, &ws.ascan, &ws.aspan}) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  ws.cap_anbt = 0;
+  hipError_t e;
+  if ((e = hipMalloc(&ws.aoff, (size_t)AFF_LMAX * (nbt + 1) * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&ws.acnt, (nbt + 1) * 4)) != hipSuccess) return e;
+  if ((e = hipMalloc(&ws.ascan, scan_scratch_words(nbt + 1) * 4 + 64)) != hipSuccess) return e;
+  if ((e = hipMalloc(&ws.aspan, MAX_SPAN_BLOCKS * 4)) != hipSuccess) return e;
+  ws.cap_anbt = nbt;
+  return hipSuccess;
+}
 hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offsets, size_t nbt, size_t Emax, int pre,
                          uint32_t W, uint32_t src_off, const int32_t* idx, uint32_t* pos, uint32_t* scan_scratch,
                          uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st);

@@ -431,11 +431,12 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   constexpr int PW = F::PACKED_WORDS;
   constexpr bool G1 = std::is_same<C, G1Ops>::value;
   constexpr int NW = sizeof(typename F::T) / 4;    // raw limb words per coordinate (G1: 14)
-  constexpr int NQ = G1 ? NW / 2 : 2 * PW / 4;     // 16-byte pieces per base (G1: up to 7)
+  constexpr int NQ = NW / 2;                       // 16-byte pieces per raw-limb base (G1 7, G2 14)
   // G1 window-table records hold raw limbs (G1_TABLE_REC, 7 pieces, no unpacking), and so do the
-  // batch-affine levels' records (G1_AFF_REC: read in order, entries == null; a record of the
-  // point at infinity, AFF_IDENT, is skipped); plain vectors are packed (6 pieces)
-  const bool limbs = G1 && (rec == G1_TABLE_REC || rec == G1_AFF_REC);
+  // batch-affine levels' records (G1_AFF_REC / G2_AFF_REC: read in order, entries == null; a
+  // record of the point at infinity, AFF_IDENT in word 13, is skipped); plain vectors and G2
+  // tables are packed (6 / 12 pieces)
+  const bool limbs = G1 ? (rec == G1_TABLE_REC || rec == G1_AFF_REC) : rec == G2_AFF_REC;
   const int nq = limbs ? NQ : 2 * PW / 4;
   __shared__ uint4 pre[4][NQ][64];
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
@@ -493,7 +494,7 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
       a.y = F::unpack(w + PW);
     }
     if (e_cur & 0x80000000u) a = C::neg_affine(a);
-    const bool skip = limbs && (w[NW - 1] & AFF_IDENT);  // (a level record of the point at infinity)
+    const bool skip = limbs && (w[13] & AFF_IDENT);  // (a level record of the point at infinity)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
     if (j + 1 < end) {
       issue(e_next);
@@ -556,14 +557,14 @@ void fit_segments_E(MsmShape& sh, size_t E) {
 template <class C>
 AffinePlan affine_plan_for(const MsmWorkspace<C>& ws, size_t n, const MsmShape& sh) {
   AffinePlan pl;
-  if constexpr (std::is_same<C, G1Ops>::value) {
-    if (ws.aff && sh.rec == (int)G1_TABLE_REC && n > 0) {
-      pl = affine_plan_g1(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves);
-      if (pl.levels) {
-        MsmShape s2 = sh;
-        fit_segments_E<C>(s2, pl.Eb[pl.levels]);
-        pl.S = s2.S;
-      }
+  constexpr bool G1 = std::is_same<C, G1Ops>::value;
+  if (ws.aff && sh.rec == (int)(G1 ? G1_TABLE_REC : G2_TABLE_REC) && n > 0) {
+    pl = G1 ? affine_plan_g1(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves)
+            : affine_plan_g2(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves);
+    if (pl.levels) {
+      MsmShape s2 = sh;
+      fit_segments_E<C>(s2, pl.Eb[pl.levels]);
+      pl.S = s2.S;
     }
   }
   return pl;
@@ -718,20 +719,22 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
-    if constexpr (std::is_same<C, G1Ops>::value) {
+    {
       const AffinePlan pl = affine_plan_for<C>(ws, n, sh);
       if (pl.levels) {  // batch-affine levels, then the XYZZ accumulation over the last level's records
         // (the level buffers are the context's: held from their sizing to the last launch reading them)
         std::lock_guard<std::mutex> lk(ws.aff->mu);
         const uint32_t* fin = nullptr;
-        hipError_t e = affine_levels_g1(ws, st, d_bases, rec, pl, nbt, &fin);
+        hipError_t e;
+        if constexpr (std::is_same<C, G1Ops>::value) e = affine_levels_g1(ws, st, d_bases, rec, pl, nbt, &fin);
+        else e = affine_levels_g2(ws, st, d_bases, rec, pl, nbt, &fin);
         if (e != hipSuccess) return e;
         const size_t fsegs = (pl.Eb[pl.levels] + pl.S - 1) / pl.S;
         if ((e = ws.grow(0, 0, fsegs + 1, 0)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(fsegs, 256)), dim3(256), 0, st,
                            (const uint32_t*)nullptr, ws.aoff + (size_t)(pl.levels - 1) * (nbt + 1), (uint32_t)nbt,
-                           fin, G1_AFF_REC, (uint32_t)pl.S, 0u, (uint32_t)nbt, ws.bucket_sums, ws.conts,
-                           ws.cont_bucket);
+                           fin, std::is_same<C, G1Ops>::value ? G1_AFF_REC : G2_AFF_REC, (uint32_t)pl.S, 0u,
+                           (uint32_t)nbt, ws.bucket_sums, ws.conts, ws.cont_bucket);
         if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
         return hipGetLastError();
       }

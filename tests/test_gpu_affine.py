@@ -91,6 +91,47 @@ def test_affine_exceptional_pairs_in_table_buckets(ctx):
         assert got == want
 
 
+def test_affine_exceptional_pairs_g2(ctx):
+    """The same for G2: b_g2 replaced by multiples of the G2 generator from {11, -11, 29, 22}, a
+    table multiexp over it (level 0 from the packed G2 table records, Fp2 affine levels, one Fp
+    inversion of the norm per thread) == sum(e_i k_i) * G2 (oracle) and the XYZZ-only result."""
+    bh = _bh()
+    from oracle import bellman as bm
+    from oracle import bls12_381 as bls
+    from params_bytes import split_params
+    E = bm.BLS12_381
+    G = E.G2
+    gen = bls.G2.generator()
+    rounds = (1 << 17) - 1
+    raw = bh.Parameters.chain(ctx, rounds).write()
+    sp = split_params(raw)
+    n = sp["b_g2_len"]
+    ks = [11, R - 11, 29, 22]
+    enc = {k: bls.g2_to_uncompressed(G.to_affine(G.mul(gen, k))) for k in ks}
+    pick = [ks[(i * 5 + (i >> 6)) % 4] for i in range(n)]
+    start = raw.index(sp["b_g2"])
+    crafted = raw[:start] + b"".join(enc[k] for k in pick) + raw[start + len(sp["b_g2"]):]
+    params = bh.Parameters.read(ctx, crafted, checked=False)
+    w = bh.Witness.chain(ctx, rounds)
+    params.prepare(w)
+    B2 = params.vector(bh.BH_VEC_B_G2)
+    asg = bh.chain_assignment(rounds)
+    off = bh.DensityWords(asg["b_input_density"], asg["inputs"].shape[0]).total()
+    m = n - off
+    rng = random.Random(8)
+    e1, e2 = rng.randrange(R), rng.randrange(R)
+    for exps in ([e1 if i % 3 else e2 for i in range(m)], [e2] * m):
+        want_k = sum(e * k for e, k in zip(exps, pick[off:])) % R
+        want = bls.g2_to_uncompressed(G.to_affine(G.mul(gen, want_k)))
+        ex = _exps_array(exps)
+        with env(**FORCE):
+            got = bh.multiexp_async(ctx, B2, off, None, ex).wait()
+        with env(BH_AFFINE=0):
+            xyzz = bh.multiexp_async(ctx, B2, off, None, ex).wait()
+        assert xyzz == want
+        assert got == want
+
+
 @pytest.mark.parametrize("rounds", [(1 << 15) - 1, (1 << 16) - 1])
 def test_affine_forced_levels_proof_equals_xyzz(ctx, rounds):
     """Whole proofs with window tables: forced affine levels (several per multiexp at these

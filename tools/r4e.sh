@@ -1,0 +1,7 @@
+# round 4: affine G1+G2 tests, parity subset with levels on, bench A/B (G2 only, both), profile
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && O=gpurun_out/${TAG:-r4e} && mkdir -p $O &&
+timeout -k 10 400 python -u -m pytest tests/test_gpu_affine.py -x -v --timeout 200 --timeout-method thread > $O/affine.log 2>&1 &&
+BH_AFFINE=1 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "window_tables_match or prove_batch_equals or c5_batch or degenerate or g2_msm" > $O/parity.log 2>&1 &&
+BH_AFFINE_G2=1 timeout -k 10 300 python -u bench.py --cpu-baseline 0 --c5 0 --dropin 0 --seam 0 --steps 10 --warmup 3 > $O/bench_g2.log 2>&1 &&
+BH_AFFINE=1 timeout -k 10 300 python -u bench.py --cpu-baseline 0 --c5 0 --dropin 0 --seam 0 --steps 10 --warmup 3 > $O/bench_both.log 2>&1 &&
+BH_AFFINE=1 SQW=1 TAG=${TAG:-r4e}/prof PSTEPS=2 bash tools/r4_prof.sh
