@@ -138,6 +138,7 @@ def _load():
         "bh_scalars_free": (I, [P]),
         "bh_multiexp_submit_scalars": (I, [P, P, S, P, S, P, P]),
         "bh_scalars_sync": (I, [P]),
+        "bh_scratch_report": (I, [P, P, S, ctypes.c_char_p, S]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -163,7 +164,7 @@ EXPORTED_SYMBOLS = [
     "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
     "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch", "bh_verify_proof", "bh_verify_batch",
     "bh_params_vector", "bh_scalars_upload", "bh_compute_h_scalars", "bh_scalars_len", "bh_scalars_free",
-    "bh_multiexp_submit_scalars", "bh_scalars_sync",
+    "bh_multiexp_submit_scalars", "bh_scalars_sync", "bh_scratch_report",
 ]
 BH_VEC_H, BH_VEC_L, BH_VEC_A, BH_VEC_B_G1, BH_VEC_B_G2 = range(5)
 PARTIAL_BYTES = 960
@@ -281,6 +282,18 @@ class Context:
         out = (ctypes.c_double * 13)()
         _check(_lib.bh_last_stats(self.h, out, 13))
         return list(out)
+
+    def scratch_report(self):
+        """bh_scratch_report: the scratch budget of the library's kernels against the device limit."""
+        out = (ctypes.c_uint64 * 8)()
+        name = ctypes.create_string_buffer(64)
+        _check(_lib.bh_scratch_report(self.h, out, 8, name, 64))
+        keys = ["limit_max", "limit_current", "worst_bytes_per_lane", "worst_per_queue", "queues", "total_need",
+                "fits", "kernels_checked"]
+        d = dict(zip(keys, list(out)))
+        d["fits"] = bool(d["fits"])
+        d["worst_kernel"] = name.value.decode()
+        return d
 
     def close(self):
         if self.h:

@@ -679,6 +679,7 @@ const char* bh_status_string(bh_status s) {
     case BH_ERR_INVALID_ARGUMENT: return "invalid argument";
     case BH_ERR_INVALID_ENCODING: return "invalid point encoding";
     case BH_ERR_NOT_IN_SUBGROUP: return "point is not in the prime-order subgroup";
+    case BH_ERR_SCRATCH_LIMIT: return "a kernel's scratch would exceed the device's scratch limit";
     case BH_ERR_NOT_ON_CURVE: return "point not on curve";
     case BH_ERR_OUT_OF_MEMORY: return "device out of memory";
     case BH_ERR_HIP: return "HIP runtime error";
@@ -961,6 +962,7 @@ bh_status bh_multiexp(bh_ctx* ctx, const bh_srs* bases, size_t base_offset, cons
   if (n > 0x7fffffffull) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
   BH_TRY_HIP(hipSetDevice(ctx->device));
+  if (bh_status sc = scratch_check(ctx)) return sc;  // rather than an abort inside the runtime
   // error semantics first (needs canonical exponents only when identity bases are reachable)
   std::vector<uint64_t> canon;
   const uint64_t* ex_c = exponents;

@@ -10,6 +10,7 @@
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
+#include <string>
 #include <thread>
 #include <tuple>
 #include <vector>
@@ -284,6 +285,10 @@ struct bh_ctx {
   // submit never waits behind a proof holding mu)
   std::shared_ptr<bh_job_registry> jobs = std::make_shared<bh_job_registry>();
   std::mutex mu;
+  // scratch budget (scratch.cpp), computed once: see bh_scratch_report
+  bool scratch_done = false;
+  uint64_t scratch_rep[8] = {};
+  std::string scratch_worst;
 };
 
 void bh_ctx_release_jobs(bh_ctx* ctx);
@@ -336,6 +341,11 @@ struct Exchanger {
 std::unique_ptr<Exchanger> rccl_exchanger(bh_comm* c);
 // smallest rank count that uses the distributed H pipeline (BH_DIST_H_MIN, default 4)
 size_t dist_h_min_ranks();
+// the scratch budget check (scratch.cpp): BH_ERR_SCRATCH_LIMIT when the worst spilling kernel's
+// per-queue scratch times the context's queues exceeds the device's scratch limit (thread-safe;
+// computed once per context)
+bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst);
+bh_status scratch_check(bh_ctx* ctx);
 int comm_rank(const bh_comm* c);
 int comm_size(const bh_comm* c);
 }  // namespace bh

@@ -11,6 +11,7 @@
 // or, for tests and rehearsal, with N virtual ranks on one device
 // (bh_prove_witness_partials_local).
 #pragma once
+#include "kinfo.h"
 #include <functional>
 
 #include "api_internal.h"
@@ -34,6 +35,8 @@ bh_status dist_h_phase1(bh_ctx* ctx, DistH& d, const uint32_t* abc_full, hipStre
 bh_status dist_h_phase2(bh_ctx* ctx, DistH& d, hipStream_t st);                            // send work -> recv
 bh_status dist_h_phase3(bh_ctx* ctx, DistH& d, hipStream_t st);                            // send recv[0] -> work[0]
 bh_status dist_h_final(bh_ctx* ctx, DistH& d, hipStream_t st);                             // -> hbuf, hidx
+// the distributed-H unit's kernels (scratch budget, scratch.cpp)
+void dist_kernels(std::vector<KernInfo>& v);
 // whole pipeline with an exchange callback, stream-ordered on st
 bh_status dist_h_run(bh_ctx* ctx, DistH& d, const uint32_t* abc_full, const HExchange& ex, hipStream_t st);
 

@@ -278,4 +278,15 @@ bh_status dist_h_run(bh_ctx* ctx, DistH& d, const uint32_t* abc_full, const HExc
   return dist_h_final(ctx, d, st);
 }
 
+void dist_kernels(std::vector<KernInfo>& v) {
+  v.push_back({"k_dist_mid<2>", (const void*)k_dist_mid<2>, 256, 0});
+  v.push_back({"k_dist_mid<4>", (const void*)k_dist_mid<4>, 256, 0});
+  v.push_back({"k_dist_mid<8>", (const void*)k_dist_mid<8>, 256, 0});
+  v.push_back({"k_dist_mid<16>", (const void*)k_dist_mid<16>, 256, 0});
+  v.push_back({"k_dist_final<2>", (const void*)k_dist_final<2>, 256, 0});
+  v.push_back({"k_dist_final<4>", (const void*)k_dist_final<4>, 256, 0});
+  v.push_back({"k_dist_final<8>", (const void*)k_dist_final<8>, 256, 0});
+  v.push_back({"k_dist_final<16>", (const void*)k_dist_final<16>, 256, 0});
+}
+
 }  // namespace bh

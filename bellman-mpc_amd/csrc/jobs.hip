@@ -271,7 +271,7 @@ bh_status submit_check(bh_ctx* ctx, const bh_srs* bases, const uint64_t* density
                        size_t n) {
   if (density_words && density_len != n) return BH_ERR_DENSITY_SIZE_MISMATCH;  // the reference asserts
   if (n > 0x7fffffffull || !bases->ctx || bases->ctx->device != ctx->device) return BH_ERR_INVALID_ARGUMENT;
-  return BH_OK;
+  return scratch_check(ctx);  // rather than an abort inside the runtime
 }
 
 }  // namespace

@@ -7,6 +7,7 @@
 #include <mutex>
 
 #include "curve.cuh"
+#include "kinfo.h"
 
 namespace bh {
 
@@ -173,6 +174,13 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
                     int max_span = -1, hipEvent_t acc_done = nullptr, const uint32_t* d_span_words = nullptr);
 
 size_t scan_scratch_words(size_t n);
+// the kernels each MSM unit emits (scratch budget, scratch.cpp)
+template <class C>
+void msm_acc_kernels(std::vector<KernInfo>& v);
+template <class C>
+void msm_back_kernels(std::vector<KernInfo>& v);
+void aff_kernels_g1(std::vector<KernInfo>& v);
+void aff_kernels_g2(std::vector<KernInfo>& v);
 // max over buckets of (last segment - first segment) for segment length S: the
 // continuation-tree depth msm_back needs.  Each of max_span_blocks(nbt) workgroups writes its
 // own maximum to d_words[b] and the (pinned) h_words receive them, stream-ordered; the host takes

@@ -13,4 +13,5 @@ template hipError_t msm_sort<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uin
                                      uint32_t, const MsmShape&);
 template hipError_t msm_accumulate<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,
                                            MsmTiming*);
+template void msm_acc_kernels<G1Ops>(std::vector<KernInfo>&);
 }  // namespace bh

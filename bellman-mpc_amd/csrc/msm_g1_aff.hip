@@ -85,4 +85,9 @@ hipError_t affine_levels_g1(MsmWorkspace<G1Ops>& ws, hipStream_t st, const uint3
                                    k_aff_bwd_g1, final_pts);
 }
 
+void aff_kernels_g1(std::vector<KernInfo>& v) {
+  v.push_back({"k_aff_fwd_g1", (const void*)k_aff_fwd_g1, 256, 0});
+  v.push_back({"k_aff_bwd_g1", (const void*)k_aff_bwd_g1, 256, 0});
+}
+
 }  // namespace bh

@@ -20,4 +20,5 @@ template hipError_t msm_window_sums<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, co
 template hipError_t msm_front<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
 template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, size_t, const MsmShape&, typename G1Ops::P*, int, hipEvent_t, const uint32_t*);
+template void msm_back_kernels<G1Ops>(std::vector<KernInfo>&);
 }  // namespace bh

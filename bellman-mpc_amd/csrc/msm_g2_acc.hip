@@ -15,4 +15,5 @@ template hipError_t msm_sort<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uin
                                      uint32_t, const MsmShape&);
 template hipError_t msm_accumulate<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,
                                            MsmTiming*);
+template void msm_acc_kernels<G2Ops>(std::vector<KernInfo>&);
 }  // namespace bh

@@ -36,4 +36,11 @@ hipError_t affine_levels_g2(MsmWorkspace<G2Ops>& ws, hipStream_t st, const uint3
                                    k_aff_fwd_g2<false>, k_aff_bwd_g2<false>, final_pts);
 }
 
+void aff_kernels_g2(std::vector<KernInfo>& v) {
+  v.push_back({"k_aff_fwd_g2<packed>", (const void*)k_aff_fwd_g2<true>, 256, 0});
+  v.push_back({"k_aff_bwd_g2<packed>", (const void*)k_aff_bwd_g2<true>, 256, 0});
+  v.push_back({"k_aff_fwd_g2", (const void*)k_aff_fwd_g2<false>, 256, 0});
+  v.push_back({"k_aff_bwd_g2", (const void*)k_aff_bwd_g2<false>, 256, 0});
+}
+
 }  // namespace bh

@@ -20,4 +20,5 @@ template hipError_t msm_window_sums<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, co
 template hipError_t msm_front<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, const uint32_t*, size_t,
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
 template hipError_t msm_back<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, size_t, const MsmShape&, typename G2Ops::P*, int, hipEvent_t, const uint32_t*);
+template void msm_back_kernels<G2Ops>(std::vector<KernInfo>&);
 }  // namespace bh

@@ -874,6 +874,24 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
 }
 
 template <class C>
+void msm_acc_kernels(std::vector<KernInfo>& v) {
+  v.push_back({std::is_same<C, G1Ops>::value ? "k_accumulate_pf<G1>" : "k_accumulate_pf<G2>",
+               (const void*)k_accumulate_pf<C>, 256, 0});
+}
+template <class C>
+void msm_back_kernels(std::vector<KernInfo>& v) {
+  constexpr bool G2 = sizeof(typename C::P) > 256;
+  const size_t P = sizeof(typename C::P);
+  const int B = G2 ? 128 : 256, BT = (int)reduce_block_max(G2);
+  v.push_back({G2 ? "k_reduce_blocks<G2>" : "k_reduce_blocks<G1>", (const void*)k_reduce_blocks<C>, BT, BT * P});
+  v.push_back({G2 ? "k_reduce_window<G2>" : "k_reduce_window<G1>", (const void*)k_reduce_window<C>, BT,
+               2 * BT * P});
+  v.push_back({G2 ? "k_cont_seq<G2>" : "k_cont_seq<G1>", (const void*)k_cont_seq<C, 4>, B, B * P});
+  v.push_back({G2 ? "k_cont_long<G2>" : "k_cont_long<G1>", (const void*)k_cont_long<C>, B, B * P});
+  v.push_back({G2 ? "k_cont_treeF<G2>" : "k_cont_treeF<G1>", (const void*)k_cont_treeF<C, 4>, 256, 0});
+}
+
+template <class C>
 hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_bases, const uint32_t* d_scalars,
                            size_t n, const int32_t* d_idx, uint32_t base_offset, const MsmShape& sh,
                            MsmTiming* timing) {

@@ -1,5 +1,6 @@
 // Host interface of the device NTT family (ntt.hip).
 #pragma once
+#include "kinfo.h"
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -47,5 +48,7 @@ void launch_pointwise(uint32_t* a, const uint32_t* b, const uint32_t* c, size_t 
 void launch_fr_convert(const uint32_t* in, uint32_t* out, size_t n, const FrConst& C, int reduce, hipStream_t st);
 void launch_expand_table(uint32_t* tab, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits,
                          hipStream_t st);
+// the NTT unit's kernels (scratch budget, scratch.cpp)
+void ntt_kernels(std::vector<KernInfo>& v);
 
 }  // namespace bh

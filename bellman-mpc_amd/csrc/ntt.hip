@@ -371,4 +371,9 @@ void launch_level_table(uint32_t* lv, int L, const uint32_t* tw, hipStream_t st)
   hipLaunchKernelGGL(k_level_table, dim3(nb((size_t)1 << L, 256)), dim3(256), 0, st, lv, L, tw);
 }
 
+void ntt_kernels(std::vector<KernInfo>& v) {
+  v.push_back({"k_ntt_pass<DIF>", (const void*)k_ntt_pass<true>, NTT_T, 0});
+  v.push_back({"k_ntt_pass<DIT>", (const void*)k_ntt_pass<false>, NTT_T, 0});
+}
+
 }  // namespace bh

@@ -657,6 +657,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                        Jac<Fp> res1[6], Jac<bh::Fp2> res2[2], Exchanger* ex = nullptr, bool may_build = true,
                        UploadSync* up = nullptr) {
   const auto t0 = std::chrono::steady_clock::now();
+  if (bh_status sc = scratch_check(ctx)) return sc;  // rather than an abort inside the runtime
   bh_params* mparams = const_cast<bh_params*>(params);
   // The proof reads the Parameters' window tables under a shared lock (taken below).  Declared
   // before the drain guard so that on an error return the streams are drained BEFORE the lock
@@ -779,7 +780,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   // the public-input multiexps on a host thread (HOST_INPUT_MSM_MAX); BH_HOST_INPUTS=0: on the
   // device like the others (A/B experiments)
-  static const bool host_inputs_on = [] {
+  // (read per proof: tests run the device branch of small input counts with BH_HOST_INPUTS=0)
+  const bool host_inputs_on = [] {
     const char* e = getenv("BH_HOST_INPUTS");
     return !(e && e[0] == '0');
   }();

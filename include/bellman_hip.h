@@ -63,6 +63,7 @@ typedef int bh_status;
 #define BH_ERR_NOT_ON_CURVE 12          /* the checked decoders' InvalidData (mod.rs:292-400) */
 #define BH_ERR_NOT_IN_SUBGROUP 14       /* same reference error: not torsion-free */
 #define BH_ERR_OUT_OF_MEMORY 13
+#define BH_ERR_SCRATCH_LIMIT 15          /* a kernel's spill scratch would exceed the device's limit (no reference counterpart) */
 #define BH_ERR_HIP 100                   /* HIP runtime / device failure */
 
 #define BH_G1 1
@@ -313,6 +314,17 @@ bh_status bh_last_timings(const bh_ctx* ctx, double out[10]);
  * read (each distinct table once: for a shard, its own slices); n entries are written (missing
  * ones 0). */
 bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
+
+/* ---- scratch budget (no reference counterpart: a guard the device needs).  A spilling kernel's
+ * scratch is provisioned per hardware queue for the waves it can have in flight, out of one
+ * device-wide amount; exceeding it aborts inside the runtime (HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+ * The library checks its kernels (private segment per lane x 64 x resident waves, times the
+ * queues a context runs them on) against the device limit before every proof and multiexp, which
+ * return BH_ERR_SCRATCH_LIMIT instead.  out[0..n): [0] device scratch limit (bytes, shared by all
+ * queues; 0 unknown), [1] current per-queue threshold, [2] worst private segment (bytes/lane),
+ * [3] its per-queue need, [4] queues counted, [5] total need, [6] fits (1/0), [7] kernels
+ * checked; worst_kernel (optional, cap bytes): that kernel's name. */
+bh_status bh_scratch_report(bh_ctx* ctx, uint64_t* out, size_t n, char* worst_kernel, size_t cap);
 
 #ifdef __cplusplus
 }

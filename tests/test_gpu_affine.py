@@ -201,3 +201,15 @@ def test_witness_of_ones_tail_latency(ctx):
         xyzz = bh.multiexp_async(ctx, L, 0, None, ex).wait()
     assert got == got2 == xyzz == want
     assert dt < 0.5, f"{dt * 1e3:.1f} ms"
+
+
+def test_scratch_budget_report(ctx):
+    """the scratch the spilling kernels need (private segment x 64 lanes x resident waves
+    per queue, times the context's queues) is checked against the device limit before proofs and
+    multiexps (BH_ERR_SCRATCH_LIMIT instead of an HSA abort); the report names the worst kernel."""
+    r = ctx.scratch_report()
+    assert r["kernels_checked"] >= 20
+    assert r["worst_bytes_per_lane"] > 0 and r["worst_kernel"] != "-"
+    assert r["total_need"] == r["worst_per_queue"] * r["queues"]
+    assert r["fits"]
+    print("scratch report:", r)
