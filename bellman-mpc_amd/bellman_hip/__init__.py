@@ -285,11 +285,11 @@ class Context:
 
     def scratch_report(self):
         """bh_scratch_report: the scratch budget of the library's kernels against the device limit."""
-        out = (ctypes.c_uint64 * 8)()
+        out = (ctypes.c_uint64 * 10)()
         name = ctypes.create_string_buffer(64)
-        _check(_lib.bh_scratch_report(self.h, out, 8, name, 64))
+        _check(_lib.bh_scratch_report(self.h, out, 10, name, 64))
         keys = ["limit_max", "limit_current", "worst_bytes_per_lane", "worst_per_queue", "queues", "total_need",
-                "fits", "kernels_checked"]
+                "fits", "kernels_checked", "worst_per_queue_resident", "live_contexts"]
         d = dict(zip(keys, list(out)))
         d["fits"] = bool(d["fits"])
         d["worst_kernel"] = name.value.decode()

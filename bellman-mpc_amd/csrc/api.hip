@@ -712,9 +712,17 @@ __attribute__((constructor)) static void bh_hw_queues() {
 }
 
 static std::atomic<int> g_masked_ctxs[64];  // live CU-masked contexts per device (0 or 1)
-static void release_mask(bh_ctx* c) {
+static std::atomic<int> g_live_ctxs[64];    // live contexts per device (scratch report)
+}  // extern "C"
+namespace bh {
+int live_contexts(int device) { return device >= 0 && device < 64 ? g_live_ctxs[device].load() : 0; }
+}  // namespace bh
+extern "C" {
+static void release_mask(bh_ctx* c) {  // (every path that deletes a created context)
   if (c->cu_masked) g_masked_ctxs[c->device].fetch_sub(1);
   c->cu_masked = false;
+  if (c->counted) g_live_ctxs[c->device].fetch_sub(1);
+  c->counted = false;
 }
 
 bh_status bh_ctx_create(int device, bh_ctx** out) {
@@ -725,13 +733,17 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   bh_ctx* c = new bh_ctx();
   c->device = device;
   c->attach_affine();
+  if (device < 64) {
+    g_live_ctxs[device]++;
+    c->counted = true;
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess) {
-    delete c;
+    release_mask(c); delete c;
     return BH_ERR_HIP;
   }
   int prio_lo = 0, prio_hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { delete c; return BH_ERR_HIP; }
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   // side streams (sorts, H pipeline, reduction tails) at high priority; BH_SIDE_PRIORITY=0
   // puts them at the default priority (A/B experiments)
   const char* pe = getenv("BH_SIDE_PRIORITY");
@@ -739,7 +751,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess) {
-    delete c;
+    release_mask(c); delete c;
     return BH_ERR_HIP;
   }
   // The reduction tails run on a quarter of the CUs (every 4th, a CU mask): their waves are

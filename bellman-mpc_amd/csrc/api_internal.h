@@ -287,7 +287,8 @@ struct bh_ctx {
   std::mutex mu;
   // scratch budget (scratch.cpp), computed once: see bh_scratch_report
   bool scratch_done = false;
-  uint64_t scratch_rep[8] = {};
+  bool counted = false;  // in api.hip's live-context count of its device
+  uint64_t scratch_rep[10] = {};
   std::string scratch_worst;
 };
 
@@ -344,7 +345,9 @@ size_t dist_h_min_ranks();
 // the scratch budget check (scratch.cpp): BH_ERR_SCRATCH_LIMIT when the worst spilling kernel's
 // per-queue scratch times the context's queues exceeds the device's scratch limit (thread-safe;
 // computed once per context)
-bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst);
+bh_status scratch_report(bh_ctx* ctx, uint64_t out[10], std::string* worst);
+// live contexts of a device (api.hip)
+int live_contexts(int device);
 bh_status scratch_check(bh_ctx* ctx);
 int comm_rank(const bh_comm* c);
 int comm_size(const bh_comm* c);

@@ -49,9 +49,11 @@ hsa_status_t visit_agent(hsa_agent_t a, void* p) {
 }  // namespace
 
 // out: [0] device scratch limit (bytes, shared by all queues; 0 = unknown), [1] current per-queue
-// threshold, [2] worst bytes/lane, [3] its per-queue need (bytes), [4] queues counted, [5] total
-// need, [6] fits (1/0), [7] kernels checked
-bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst) {
+// threshold, [2] worst bytes/lane, [3] its per-queue need at the scratch-slot bound (bytes),
+// [4] queues counted, [5] the context's total need, [6] fits (1/0), [7] kernels checked, [8] the
+// worst kernel's per-queue need at its occupancy, [9] live contexts on the device (the limit is
+// shared by all of them: [5] x [9] bounds a device full of such contexts)
+bh_status scratch_report(bh_ctx* ctx, uint64_t out[10], std::string* worst) {
   static std::mutex mu;  // (computed once per context, by whichever thread asks first)
   std::lock_guard<std::mutex> lk(mu);
   if (ctx->scratch_done) {
@@ -80,7 +82,9 @@ bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst) {
   dist_kernels(ks);
   const uint64_t cus = (uint64_t)std::max(prop.multiProcessorCount, 1);
   const uint64_t slots_per_cu = 32;  // KFD max_slots_scratch_cu (profiles/r03_kfd_queue_props.txt)
-  uint64_t worst_need = 0, worst_lane = 0;
+  // per queue: at the scratch-slot bound (what the runtime may reserve for a large dispatch:
+  // 32 waves per CU) and at the kernel's occupancy (the waves resident at once)
+  uint64_t worst_need = 0, worst_lane = 0, worst_resident = 0;
   std::string wname = "-";
   for (const KernInfo& k : ks) {
     hipFuncAttributes a;
@@ -91,10 +95,12 @@ bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k.fn, k.block, k.lds) != hipSuccess || blocks < 1)
       blocks = 1;
     const uint64_t waves_cu = std::min<uint64_t>(slots_per_cu, (uint64_t)blocks * ((k.block + 63) / 64));
-    const uint64_t need = ((lane + 15) / 16 * 16) * 64 * waves_cu * cus;
+    const uint64_t per_lane = (lane + 15) / 16 * 16;
+    const uint64_t need = per_lane * 64 * slots_per_cu * cus;
     if (need > worst_need) {
       worst_need = need;
       worst_lane = lane;
+      worst_resident = per_lane * 64 * waves_cu * cus;
       wname = k.name;
     }
   }
@@ -111,6 +117,8 @@ bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst) {
   ctx->scratch_rep[5] = total;
   ctx->scratch_rep[6] = fits ? 1 : 0;
   ctx->scratch_rep[7] = ks.size();
+  ctx->scratch_rep[8] = worst_resident;
+  ctx->scratch_rep[9] = (uint64_t)std::max(1, live_contexts(ctx->device));
   ctx->scratch_worst = wname;
   ctx->scratch_done = true;
   memcpy(out, ctx->scratch_rep, sizeof(ctx->scratch_rep));
@@ -119,7 +127,7 @@ bh_status scratch_report(bh_ctx* ctx, uint64_t out[8], std::string* worst) {
 }
 
 bh_status scratch_check(bh_ctx* ctx) {
-  uint64_t r[8];
+  uint64_t r[10];
   bh_status s = scratch_report(ctx, r, nullptr);
   if (s) return s;
   return r[6] ? BH_OK : BH_ERR_SCRATCH_LIMIT;
@@ -129,11 +137,11 @@ bh_status scratch_check(bh_ctx* ctx) {
 
 extern "C" bh_status bh_scratch_report(bh_ctx* ctx, uint64_t* out, size_t n, char* worst_kernel, size_t cap) {
   if (!ctx || (!out && n)) return BH_ERR_INVALID_ARGUMENT;
-  uint64_t r[8];
+  uint64_t r[10];
   std::string w;
   bh_status s = bh::scratch_report(ctx, r, &w);
   if (s) return s;
-  for (size_t i = 0; i < n && i < 8; i++) out[i] = r[i];
+  for (size_t i = 0; i < n && i < 10; i++) out[i] = r[i];
   if (worst_kernel && cap) {
     const size_t m = std::min(cap - 1, w.size());
     memcpy(worst_kernel, w.data(), m);

@@ -322,8 +322,10 @@ bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
  * queues a context runs them on) against the device limit before every proof and multiexp, which
  * return BH_ERR_SCRATCH_LIMIT instead.  out[0..n): [0] device scratch limit (bytes, shared by all
  * queues; 0 unknown), [1] current per-queue threshold, [2] worst private segment (bytes/lane),
- * [3] its per-queue need, [4] queues counted, [5] total need, [6] fits (1/0), [7] kernels
- * checked; worst_kernel (optional, cap bytes): that kernel's name. */
+ * [3] its per-queue need at the scratch-slot bound (32 waves per CU), [4] queues counted, [5] the
+ * context's total need, [6] fits (1/0), [7] kernels checked, [8] the worst kernel's per-queue need
+ * at its occupancy, [9] live contexts on the device; worst_kernel (optional, cap bytes): that
+ * kernel's name. */
 bh_status bh_scratch_report(bh_ctx* ctx, uint64_t* out, size_t n, char* worst_kernel, size_t cap);
 
 #ifdef __cplusplus
