@@ -522,7 +522,7 @@ bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
     BH_TRY_HIP(tab.alloc(n * 9 * 4));
     launch_expand_table(tab.as<uint32_t>(), n, lo.as<uint32_t>(), hi.as<uint32_t>(), tb, ctx->stream);
     DevBuf& lv = dir == 0 ? d->lv_fwd : d->lv_inv;
-    BH_TRY_HIP(lv.alloc(std::max<size_t>(m, 2) * 32));
+    BH_TRY_HIP(lv.alloc(std::max<size_t>(m, 2) * 36));
     launch_level_table(lv.as<uint32_t>(), L, tab.as<uint32_t>(), ctx->stream);
     BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
   }

@@ -61,7 +61,7 @@ struct DevBuf {
 struct Domain {
   int L = -1;
   DevBuf tw_fwd, tw_inv;                  // omega^j, omega^-j, j < m/2
-  DevBuf lv_fwd, lv_inv;                  // per-level packed twiddles (launch_level_table)
+  DevBuf lv_fwd, lv_inv;                  // per-level twiddles, 9 limbs each (launch_level_table)
   DevBuf coset_lo, coset_hi;              // g^i split tables, hi folded with m^-1   (ifft -> coset)
   DevBuf icoset_lo, icoset_hi;            // g^-i split, hi folded with m^-1        (icoset)
   DevBuf gpow_lo, gpow_hi;                // g^i (no m^-1)                           (coset_fft input)

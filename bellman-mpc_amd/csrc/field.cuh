@@ -62,25 +62,37 @@ BH_DEV Fe<C> fe_one() {  // Montgomery form of 1
 }
 
 // Montgomery product, FIPS column order. Output < 2p (see header).
+// A modulus with p = 1 (mod 2^BITS) (Fr) has m_k = -acc mod 2^BITS, so acc + m_k * p_0 is acc
+// rounded up to a multiple of 2^BITS: (acc + MASK) >> BITS, no product and no 64-bit m_k.
+// DFp keeps two independent chains (a*b and m*p) per column; for Fr the compiler splits the
+// column into a fresh chain plus a 64-bit merge either way (forcing one chain through inline
+// asm costs an s_nop per mad from the hazard recogniser).
 template <class C>
 BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
   constexpr int N = C::N;
+  constexpr bool P0_ONE = C::P[0] == 1u;
+  constexpr bool TWO_CHAINS = N > 9;
   Fe<C> r;
   uint32_t m[N];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 2 * N - 1; k++) {
-    // the column's a*b products and m*p products as two independent mad chains
     uint64_t acc2 = 0;
 #pragma unroll
     for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
       acc += (uint64_t)a.v[i] * b.v[k - i];
 #pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
-      acc2 += (uint64_t)m[i] * C::P[k - i];
-    acc += acc2;
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) {
+      if (TWO_CHAINS) acc2 += (uint64_t)m[i] * C::P[k - i];
+      else acc += (uint64_t)m[i] * C::P[k - i];
+    }
+    if (TWO_CHAINS) acc += acc2;
     if (k < N) {
       m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+      if (P0_ONE) {
+        acc = (acc + C::MASK) >> C::BITS;
+        continue;
+      }
       acc += (uint64_t)m[k] * C::P[0];
     } else {
       r.v[k - N] = (uint32_t)acc & C::MASK;

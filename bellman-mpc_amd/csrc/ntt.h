@@ -30,13 +30,13 @@ struct NttEpilogue {
 
 // Transform of 2^L packed Fr (device Montgomery, < 2r) into d; the first pass reads src
 // (default: d, in place).  dif=true: natural -> bit-reversed; dif=false: bit-reversed -> natural.
-// lv: per-level packed twiddles lv[2^v + x] = omega_{2^(v+1)}^x (launch_level_table).
+// lv: per-level twiddles (9 limbs each) lv[2^v + x] = omega_{2^(v+1)}^x (launch_level_table).
 // post_lo/hi (optional): the stored element with natural index i is multiplied by
 // lo[i & mask] * hi[i >> lo_bits].
 void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t* post_lo, const uint32_t* post_hi,
                 int post_lo_bits, hipStream_t st, const uint32_t* src = nullptr,
                 const NttEpilogue& epi = NttEpilogue());
-// lv (2^L packed entries) from the unpacked full table tw (omega^j, j < 2^(L-1))
+// lv (2^L entries of 9 limbs) from the unpacked full table tw (omega^j, j < 2^(L-1))
 void launch_level_table(uint32_t* lv, int L, const uint32_t* tw, hipStream_t st);
 void launch_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo, const uint32_t* hi, int lo_bits,
                     hipStream_t st);

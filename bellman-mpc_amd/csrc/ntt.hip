@@ -26,13 +26,63 @@ static constexpr int NTT_T = 256;   // threads per workgroup
 
 struct PassArgs {
   int L, t, D;
-  const uint32_t* lv;       // per-level twiddles, packed: lv[2^v + x] = omega_{2^(v+1)}^x, x < 2^v
+  const uint32_t* lv;       // per-level twiddles, 9 limbs: lv[2^v + x] = omega_{2^(v+1)}^x, x < 2^v
   const uint32_t* src;      // loads come from src (the first pass may run out of place)
   const uint32_t* post_lo;  // optional post-scale tables
   const uint32_t* post_hi;
   int post_lo_bits;
   NttEpilogue epi;          // what the storing pass writes
 };
+
+// ---- limb-wise (carry-free) butterfly arithmetic.  A value handed to fe_mul needs neither
+// normalised limbs nor a reduced value: with limbs < 2^31.4 against a twiddle's normalised limbs
+// a column holds 9 products < 2^60.4 plus 8 m*p products < 2^58 (< 2^63.8 with the carry), and
+// an operand < 12r keeps the product < 2r (12 r^2 < 2^261 r).  So the sums and differences that
+// only feed a product skip the carry chain (1-2 VALU per limb instead of 3-4).
+// K*r with every limb below the top >= J*(2^29-1), i.e. >= a sum of J normalised limbs: J*2^29
+// added to limb i is J taken from limb i+1 (the value is unchanged)
+template <uint32_t K, uint32_t J>
+struct FrBias {
+  struct L { uint32_t v[9]; };
+  static constexpr L make() {
+    L l{};
+    for (int i = 0; i < 9; i++) {
+      int64_t c = KP<FrCfg, K>::value.v[i];
+      if (i < 8) c += (int64_t)J << 29;
+      if (i > 0) c -= J;
+      l.v[i] = (uint32_t)c;
+    }
+    return l;
+  }
+  static constexpr L value = make();
+};
+__device__ __forceinline__ DFr lw_add(const DFr& a, const DFr& b) {
+  DFr r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + b.v[l];
+  return r;
+}
+// a + K*r - b limb-wise; b's limbs must be sums of at most J normalised limbs (and its top limb
+// at most K*r's minus J: b < (K/2) r for the callers' bounds)
+template <uint32_t K, uint32_t J>
+__device__ __forceinline__ DFr lw_sub(const DFr& a, const DFr& b) {
+  DFr r;
+#pragma unroll
+  for (int l = 0; l < 9; l++) r.v[l] = a.v[l] + (FrBias<K, J>::value.v[l] - b.v[l]);
+  return r;
+}
+// carry propagation: the same value in normalised limbs (input limbs < 2^31)
+__device__ __forceinline__ DFr lw_norm(const DFr& a) {
+  DFr r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int l = 0; l < 9; l++) {
+    const uint32_t s = a.v[l] + c;
+    r.v[l] = l < 8 ? (s & FrCfg::MASK) : s;
+    c = s >> FrCfg::BITS;
+  }
+  return r;
+}
 
 // global element index of (group g, position k) for a DIF pass at stages t..t+D-1
 __device__ __forceinline__ uint32_t dif_index(const PassArgs& a, uint32_t g, uint32_t k) {
@@ -48,9 +98,10 @@ __device__ __forceinline__ uint32_t dit_index(const PassArgs& a, uint32_t g, uin
 
 // Twiddles: the butterfly of global stage u with in-level offset x uses omega_{2h}^x where h is
 // the stage's pair distance (DIT: h = 2^u, x = (k_low << t) + lo; DIF: h = 2^(L-u-1),
-// x = k_low * 2^(L-t-D) + lo).  With one packed table per level, lanes with consecutive lo
-// (consecutive groups) read consecutive 32-byte entries, and the level-0 stage (h = 1:
-// every twiddle is 1) multiplies by nothing.
+// x = k_low * 2^(L-t-D) + lo).  With one table per level, lanes with consecutive lo
+// (consecutive groups) read consecutive entries, and the level-0 stage (h = 1: every twiddle
+// is 1) multiplies by nothing.  Entries are stored as the 9 limbs (36 bytes, L2-resident at
+// the sizes that matter): an unpack per twiddle (~25 VALU) costs more than the 4 extra bytes.
 // BH_NTT_WAVES (A/B build): register budget as waves per SIMD (LDS allows 4 workgroups per CU)
 #ifdef BH_NTT_WAVES
 #define BH_NTT_ATTR __attribute__((amdgpu_waves_per_eu(BH_NTT_WAVES)))
@@ -86,7 +137,7 @@ __global__ void __launch_bounds__(NTT_T) BH_NTT_ATTR k_ntt_pass(uint32_t* data, 
   // two radix-2 stages, three twiddle loads instead of four; the same four products)
   const int lo_bits = DIF ? (a.L - a.t - D) : a.t;  // bits of the group index below the k digits
   auto twiddle = [&](int v, uint32_t klow, uint32_t g) -> DFr {  // omega_{2^(v+1)}^(klow * 2^lo_bits + lo)
-    return ld_packed(a.lv, (1u << v) + (klow << lo_bits) + (g & ((1u << lo_bits) - 1)));
+    return ld_limbs(a.lv, (1u << v) + (klow << lo_bits) + (g & ((1u << lo_bits) - 1)));
   };
   int j = 0;
   if (D & 1) {
@@ -110,7 +161,7 @@ __global__ void __launch_bounds__(NTT_T) BH_NTT_ATTR k_ntt_pass(uint32_t* data, 
         const DFr w = twiddle(v, k & ((1u << hb) - 1), g0 + gl);
         if (DIF) {
           nx = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x, y));
-          ny = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x, y), w);
+          ny = fe_mul<FrCfg>(lw_sub<4, 1>(x, y), w);
         } else {  // lazy: no conditional subtraction inside a DIT pass (see the store)
           const DFr t = fe_mul<FrCfg>(y, w);
           nx = fe_add<FrCfg>(x, t);
@@ -146,19 +197,20 @@ __global__ void __launch_bounds__(NTT_T) BH_NTT_ATTR k_ntt_pass(uint32_t* data, 
         const int v = a.L - u - 1, v2 = v - 1;
         const uint32_t m1 = (1u << hb) - 1, m2 = (1u << (hb - 1)) - 1;
         const DFr wa0 = twiddle(v, ks[0] & m1, g), wa1 = twiddle(v, ks[1] & m1, g);
-        const DFr u0 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[0], x[2]));
-        const DFr u2 = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x[0], x[2]), wa0);
-        const DFr u1 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[1], x[3]));
-        const DFr u3 = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(x[1], x[3]), wa1);
-        y[0] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u0, u1));
-        y[2] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u2, u3));
+        // inputs < 2r (normalised); the sums feeding y0/y1 and the differences feeding the
+        // products stay limb-wise (see lw_sub), y0/y2 are carried and reduced back below 2r
+        const DFr s02 = lw_add(x[0], x[2]), s13 = lw_add(x[1], x[3]);  // < 4r, limbs < 2^30
+        const DFr u2 = fe_mul<FrCfg>(lw_sub<4, 1>(x[0], x[2]), wa0);   // < 2r
+        const DFr u3 = fe_mul<FrCfg>(lw_sub<4, 1>(x[1], x[3]), wa1);
+        y[0] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(fe_add<FrCfg>(s02, s13)));  // < 8r
+        y[2] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u2, u3));                       // < 4r
         if (v2 == 0) {  // omega_2^0 = 1
-          y[1] = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(u0, u1));
-          y[3] = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(u2, u3));
+          y[1] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(fe_csub<FrCfg, 8>(lw_norm(lw_sub<8, 2>(s02, s13)))));  // < 12r
+          y[3] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(lw_norm(lw_sub<4, 1>(u2, u3))));  // < 6r
         } else {
           const DFr wb = twiddle(v2, ks[0] & m2, g);
-          y[1] = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(u0, u1), wb);
-          y[3] = fe_mul<FrCfg>(fe_sub<FrCfg, 2>(u2, u3), wb);
+          y[1] = fe_mul<FrCfg>(lw_sub<8, 2>(s02, s13), wb);  // operand < 12r, limbs < 2^31.4
+          y[3] = fe_mul<FrCfg>(lw_sub<4, 1>(u2, u3), wb);
         }
       } else {
         // stage u (distance 2^hb): (k0, k1), (k2, k3); stage u+1 (2^(hb+1)): (k0, k2), (k1, k3).
@@ -168,26 +220,28 @@ __global__ void __launch_bounds__(NTT_T) BH_NTT_ATTR k_ntt_pass(uint32_t* data, 
         // pass reduces.  v == 0 only occurs at global stage 0, on freshly loaded values (< 2r).
         const int v = u, v2 = u + 1;
         const uint32_t m1 = (1u << hb) - 1, m2 = (2u << hb) - 1;
-        DFr u0, u1, u2, u3;
+        // u0, u1 stay limb-wise (u1's top limb may wrap: it only reaches carried sums, whose
+        // values are non-negative), u2, u3 are operands of products (limb-wise, < 26r)
+        DFr a0, a1, p2, p3;
         if (v == 0) {  // omega_2^0 = 1
-          u0 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[0], x[1]));
-          u1 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[0], x[1]));
-          u2 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[2], x[3]));
-          u3 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[2], x[3]));
+          a0 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[0], x[1]));
+          a1 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[0], x[1]));
+          p2 = fe_csub<FrCfg, 2>(fe_add<FrCfg>(x[2], x[3]));
+          p3 = fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x[2], x[3]));
         } else {
           const DFr wa = twiddle(v, ks[0] & m1, g);
           const DFr t0 = fe_mul<FrCfg>(x[1], wa), t1 = fe_mul<FrCfg>(x[3], wa);
-          u0 = fe_add<FrCfg>(x[0], t0);
-          u1 = fe_sub<FrCfg, 2>(x[0], t0);
-          u2 = fe_add<FrCfg>(x[2], t1);
-          u3 = fe_sub<FrCfg, 2>(x[2], t1);
+          a0 = lw_add(x[0], t0);
+          a1 = lw_sub<2, 1>(x[0], t0);
+          p2 = lw_add(x[2], t1);
+          p3 = lw_sub<4, 1>(x[2], t1);
         }
         const DFr wb0 = twiddle(v2, ks[0] & m2, g), wb1 = twiddle(v2, ks[1] & m2, g);
-        const DFr s0 = fe_mul<FrCfg>(u2, wb0), s1 = fe_mul<FrCfg>(u3, wb1);
-        y[0] = fe_add<FrCfg>(u0, s0);
-        y[2] = fe_sub<FrCfg, 2>(u0, s0);
-        y[1] = fe_add<FrCfg>(u1, s1);
-        y[3] = fe_sub<FrCfg, 2>(u1, s1);
+        const DFr s0 = fe_mul<FrCfg>(p2, wb0), s1 = fe_mul<FrCfg>(p3, wb1);
+        y[0] = fe_add<FrCfg>(a0, s0);
+        y[2] = lw_norm(lw_sub<2, 1>(a0, s0));
+        y[1] = fe_add<FrCfg>(a1, s1);
+        y[3] = lw_norm(lw_sub<2, 1>(a1, s1));
       }
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -297,13 +351,15 @@ __global__ void __launch_bounds__(256) k_expand_table(uint32_t* tab, uint32_t n,
   for (int l = 0; l < 9; l++) tab[(size_t)j * 9 + l] = x.v[l];
 }
 
-// per-level twiddles from the full table: lv[2^v + x] = omega^(x * 2^(L-1-v)) (packed), v < L
+// per-level twiddles from the full table: lv[2^v + x] = omega^(x * 2^(L-1-v)) (9 limbs), v < L
 __global__ void __launch_bounds__(256) k_level_table(uint32_t* lv, int L, const uint32_t* tw) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e == 0 || e >= (1u << L)) return;
   const int v = 31 - __clz(e);
   const uint32_t x = e - (1u << v);
-  st_packed(lv, e, ld_limbs(tw, (size_t)x << (L - 1 - v)));
+  const DFr w = ld_limbs(tw, (size_t)x << (L - 1 - v));
+#pragma unroll
+  for (int l = 0; l < 9; l++) lv[(size_t)e * 9 + l] = w.v[l];
 }
 
 // ------------------------------------------------------------------ host side

@@ -461,6 +461,9 @@ def main():
                    "exchange": "rccl" if world > 1 else None},
         "rccl": rccl,
         "gpu_max_hw_queues": hw_queues,
+        # scratch (private segment) budget of the library's spilling kernels against the device's
+        # shared scratch limit, checked before every proof ('Scratch budget')
+        "scratch": ctx.scratch_report(),
         "per_rank_ms_per_step": per_rank_ms,
         "srs_window_tables": tables,
         "dropin": dropin,

@@ -217,6 +217,33 @@ def test_fft_roundtrip_and_linearity(ctx, logm):
     assert delta.into_coeffs() == [1] * m
 
 
+@pytest.mark.parametrize("logm", [9, 11, 16])
+def test_fft_full_range_and_extreme_values_equal_oracle(ctx, logm):
+    """The NTT butterflies keep sums and differences limb-wise (carry-free) where they only feed
+    a product, under limb and value bounds argued in csrc/ntt.hip: checked against the oracle's
+    serial_fft (domain.rs:261-303) on full-range values and on the extremes that maximise limbs
+    and values (r-1 everywhere, r-1 / 0 alternating, 2^255-ish patterns reduced mod r), over one
+    pass (2^9: odd stage count, radix-2 first stage) and two passes (2^11, 2^16)."""
+    bh = _bh()
+    from oracle import bellman as bm
+    E = bm.BLS12_381
+    m = 1 << logm
+    rng = np.random.default_rng(100 + logm)
+    cases = {
+        "random": [int.from_bytes(rng.bytes(32), "little") % R for _ in range(m)],
+        "r-1": [R - 1] * m,
+        "alternating": [(R - 1) if i % 2 == 0 else 0 for i in range(m)],
+        "high": [((1 << 255) - 1 - i) % R for i in range(m)],
+    }
+    for name, vals in cases.items():
+        for op in ("fft", "ifft", "coset_fft", "icoset_fft"):
+            d = bh.EvaluationDomain(ctx, vals)
+            getattr(d, op)()
+            o = bm.EvaluationDomain(E, list(vals))
+            getattr(o, op)()
+            assert d.into_coeffs() == [int(x) for x in o.coeffs], (name, op, logm)
+
+
 def test_compute_h_golden(ctx, golden):
     bh = _bh()
     g = golden["h_random"]
