@@ -50,6 +50,16 @@ def main():
         ms = [round((b - a) * 1e3, 2) for a, b in zip(t, t[1:])]
         print(f"rep {rep}: total {round((t[-1] - t[0]) * 1e3, 2)} ms; h_call {ms[0]} uploads {ms[1]} "
               f"submits {ms[2]} waits {ms[3:11]} assemble {ms[11]} ok {proof == want}", flush=True)
+    # prove_seam back to back (as bench.py times it) and 200 ms apart
+    for gap in (0.0, 0.2, 0.0):
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            bh.prove_seam(ctx, params, asg, r, s)
+            ts.append(round((time.perf_counter() - t0) * 1e3, 2))
+            if gap:
+                time.sleep(gap)
+        print(f"prove_seam gap {gap}s: {ts}", flush=True)
 
 
 if __name__ == "__main__":
