@@ -49,6 +49,12 @@ class Context:
         self._stats = [1.0, 0.5, 0.8, 6, 6.0 * n, 0.2, 2, 1.0 * n, 13.0 * n, 2.0 * n,
                        5 if self.tables else 0, 5, table_bytes if self.tables else 0.0]
 
+    def scratch_report(self):
+        """bh_scratch_report's keys (bellman_hip.Context.scratch_report) with a fitting budget."""
+        return {"limit_max": 1 << 33, "limit_current": 0, "worst_bytes_per_lane": 0, "worst_per_queue": 0,
+                "queues": 7, "total_need": 0, "fits": True, "kernels_checked": 0, "worst_per_queue_resident": 0,
+                "live_contexts": 1, "worst_kernel": ""}
+
     def close(self):
         pass
 
