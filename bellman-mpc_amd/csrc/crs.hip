@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(64) k_normalize(const typename C::P* pts, size
     // 1/ZZ = ZZZ / z ; 1/ZZZ = ZZ / z
     const T x = F::reduce(F::mul(p.X, F::mul(p.ZZZ, zinv)));
     const T y = F::reduce(F::mul(p.Y, F::mul(p.ZZ, zinv)));
-    if (limbs) {  // G1 window-table record (G1_TABLE_REC): raw limbs, x then y
+    if (limbs) {  // window-table record (G1_TABLE_REC / G2_TABLE_REC): raw limbs, x then y
       constexpr int NW = sizeof(T) / 4;
       const uint32_t* xw = reinterpret_cast<const uint32_t*>(&x);
       const uint32_t* yw = reinterpret_cast<const uint32_t*>(&y);
@@ -191,7 +191,7 @@ hipError_t window_table(const uint32_t* d_pts, size_t n, int c, int W, uint32_t*
     const size_t threads = (m + CHUNK - 1) / CHUNK;
     hipLaunchKernelGGL((k_normalize<C, CHUNK>), dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, st, xyzz, m,
                        prefix, d_out + i0 * (size_t)W * rec, rec,
-                       (int)(std::is_same<C, G1Ops>::value && rec == G1_TABLE_REC));
+                       (int)(std::is_same<C, G1Ops>::value ? rec == G1_TABLE_REC : rec == G2_TABLE_REC));
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -392,6 +392,9 @@ BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, cons
     }
     acc0 >>= C::BITS;
     acc1 >>= C::BITS;
+#ifdef BH_FP2_COLUMN_SB
+    __builtin_amdgcn_sched_barrier(0);  // one column's products in flight (register pressure)
+#endif
   }
   r1.v[N - 1] = (uint32_t)acc1;
   // r0's top limb is the signed remainder; add p when it is negative

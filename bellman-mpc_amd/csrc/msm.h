@@ -83,7 +83,7 @@ struct MsmTiming {
 // P + (-P) pair) has AFF_IDENT set in x's top limb word.
 constexpr uint32_t G1_AFF_REC = 28;
 constexpr uint32_t G2_AFF_REC = 56;   // (x.c0, x.c1, y.c0, y.c1: 4 x 14 raw limbs, 224 B)
-constexpr uint32_t G2_TABLE_REC = 64; // G2 window-table record: packed x, y (48 words) in a 256-B line
+constexpr uint32_t G2_TABLE_REC = 64; // G2 window-table record: raw-limb x, y (56 words, as G2_AFF_REC) in a 256-B line
 constexpr uint32_t AFF_IDENT = 0x80000000u;
 constexpr int AFF_LMAX = 8;
 

@@ -48,9 +48,8 @@ __device__ __forceinline__ DFp fp_below2p(const DFp& x) { return fe_csub<FC, 2>(
 
 // ---- group adapters: coordinate type, its operations, and the record formats
 // raw record (a level's): x then y as raw 29-bit limbs (G1: 14 + 14 words, G2: 28 + 28);
-// table record: G1 raw limbs in a 32-word line (as a level record), G2 packed (x.c0, x.c1, y.c0,
-// y.c1 as 4 x 12 words in a 64-word line).  The point-at-infinity flag is word 13 (x's first
-// coordinate's top limb) in both.
+// table record: raw limbs as a level record, in a 32-word (G1) / 64-word (G2) line.  The
+// point-at-infinity flag is word 13 (x's first coordinate's top limb) in both.
 struct G1A {
   using T = DFp;
   static constexpr int NC = 14;               // words per coordinate (raw)
@@ -78,8 +77,8 @@ struct G2A {
   static constexpr int NC = 28;
   static constexpr uint32_t REC = G2_AFF_REC;
   static constexpr int Q_RAW = 14, XQ_RAW = 7;
-  static constexpr int Q_PK = 12, XQ_PK = 6;
-  static constexpr bool TABLE_PACKED = true;
+  static constexpr int Q_PK = 14, XQ_PK = 7;  // table records (raw limbs too)
+  static constexpr bool TABLE_PACKED = false;
   static BH_DEV T mul(const T& a, const T& b) { return Fp2Ops::mul(a, b); }
   static BH_DEV T sqr(const T& a) { return Fp2Ops::sqr(a); }
   static BH_DEV T add(const T& a, const T& b) { return Fp2Ops::add(a, b); }
@@ -196,15 +195,15 @@ __device__ __forceinline__ void load_x(const uint32_t* src, uint32_t rec, uint32
     w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
   }
   ident = !PK && (w[13] & AFF_IDENT) != 0;
-  A::coord(w, PK, x);
+  A::coord(w, PK && A::TABLE_PACKED, x);
 }
 
 // x and y of record e (y negated for a negative entry)
 template <class A, bool PK>
 __device__ __forceinline__ void decode_xy(const uint32_t* w, uint32_t e, typename A::T& x, typename A::T& y) {
-  constexpr int YOFF = PK ? A::XQ_PK * 4 : A::NC;  // (packed: x is 24 words)
-  A::coord(w, PK, x);
-  A::coord(w + YOFF, PK, y);
+  constexpr int YOFF = PK ? A::XQ_PK * 4 : A::NC;  // (table record: x's pieces)
+  A::coord(w, PK && A::TABLE_PACKED, x);
+  A::coord(w + YOFF, PK && A::TABLE_PACKED, y);
   if (e >> 31) y = A::neg(y);  // p - y, in (0, p]
 }
 

@@ -1,6 +1,7 @@
 // G2 instantiation of the batch-affine bucket accumulation (msm_aff.cuh): Fp2 coordinates
 // (column-wise Karatsuba products, as in the G2 XYZZ accumulation), one Fp inversion of the norm
-// per thread.  Level 0 reads the packed G2 window-table records, the others raw-limb records.
+// per thread.  Level 0 reads the G2 window-table records (raw limbs in 64-word lines), the others
+// the level records (raw limbs, 56 words).
 #define BH_FP2_KARATSUBA 1
 #include "msm_aff.cuh"
 

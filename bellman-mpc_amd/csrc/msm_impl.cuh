@@ -413,6 +413,200 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const t
   }
 }
 
+// The G2 segment loop of k_accumulate_pf.  A G2 mixed addition held whole in registers needs
+// the accumulator (4 Fp2 = 112 words), the base (56) and madd-2008-s's temporaries at once: the
+// allocator parked ~3 600 values per addition in AGPRs (v_accvgpr_read/write, a fifth of the
+// loop's VALU instructions).  Here the accumulator's ZZ and ZZZ live in LDS between additions
+// (component-major uint4 rows, one lane per column: conflict-free), the formula is ordered so
+// that every input dies at its last use (ZZ3 = ZZ1*PP right after PP, ZZZ3 = ZZZ1*PPP right after
+// PPP, y2 read after x2's product), and the next base's prefetch is issued once y2 is read.  The
+// exceptional cases run through the same instruction stream (a separate doubling routine inlined
+// in the loop took the kernel back to 512 registers with scratch spills; out of line it needs a
+// call stack: scratch in the hot kernel).  Identity is a register flag.
+// Bounds as CurveOps::madd (MB = 2: X < 10p, Y < 4p, ZZ, ZZZ < 2p).
+#ifndef BH_G2_NO_SB
+#define G2_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define G2_SB()
+#endif
+template <class F, int NW, int NQ, bool ZZ_LDS, class Issue>
+__device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int nq, bool limbs,
+                                               const uint32_t* entries, const uint32_t* offsets, uint32_t start,
+                                               uint32_t end, uint32_t pos0, uint32_t seg, uint32_t b, uint32_t next,
+                                               bool started_here, uint32_t e_cur, uint32_t e_next, Issue& issue,
+                                               XYZZ<F>* bucket_sums, XYZZ<F>* conts) {
+  using T = typename F::T;
+  using Cv = CurveOps<F>;
+  // rows of VW-word vectors, one column per thread: uint4 rows for G2 (7 per coordinate), uint2
+  // for G1 (7: 14 words)
+  constexpr int VW = (NW % 4 == 0) ? 4 : 2;
+  constexpr int RH = NW / VW;
+  using V = typename std::conditional<VW == 4, uint4, uint2>::type;
+  // ZZZ always in LDS; ZZ too when ZZ_LDS (else a register, as X and Y)
+  __shared__ V zzz_s[RH][256];
+  __shared__ V zz_s[ZZ_LDS ? RH : 1][256];
+  T ZZr = F::zero();
+  const int t = threadIdx.x;
+  auto put_rows = [&](V (*arr)[256], const T& v) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+    for (int q = 0; q < RH; q++) {
+      V w;
+      uint32_t* d = reinterpret_cast<uint32_t*>(&w);
+#pragma unroll
+      for (int k = 0; k < VW; k++) d[k] = s[VW * q + k];
+      arr[q][t] = w;
+    }
+  };
+  auto get_rows = [&](V (*arr)[256]) {
+    T v;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+    for (int q = 0; q < RH; q++) {
+      const V w = arr[q][t];
+      const uint32_t* s = reinterpret_cast<const uint32_t*>(&w);
+#pragma unroll
+      for (int k = 0; k < VW; k++) d[VW * q + k] = s[k];
+    }
+    return v;
+  };
+  auto put_zz = [&](const T& v) {
+    if constexpr (ZZ_LDS) put_rows(zz_s, v);
+    else ZZr = v;
+  };
+  auto get_zz = [&]() {
+    if constexpr (ZZ_LDS) return get_rows(zz_s);
+    else return ZZr;
+  };
+  // coordinate `half` (0 = x, 1 = y) of the base in this lane's prefetch slot
+  auto base_coord = [&](int half) {
+    T v;
+    if (limbs) {  // raw limbs: words [half*NW, half*NW + NW) of the record
+      uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+      if constexpr (NW % 4 == 0) {  // G2: pieces [half*NW/4, half*NW/4 + NW/4)
+#pragma unroll
+        for (int q = 0; q < NW / 4; q++) {
+          const uint4 u = pre[half * (NW / 4) + q][lane];
+          d[4 * q] = u.x; d[4 * q + 1] = u.y; d[4 * q + 2] = u.z; d[4 * q + 3] = u.w;
+        }
+      } else {  // G1: x = words 0..13 (pieces 0-3), y = words 14..27 (pieces 3-6)
+        uint32_t w[2 * NW + 4];
+#pragma unroll
+        for (int q = 0; q < (2 * NW + 3) / 4; q++) {
+          if (q < (half * NW) / 4 || q > (half * NW + NW - 1) / 4) continue;
+          const uint4 u = pre[q][lane];
+          w[4 * q] = u.x; w[4 * q + 1] = u.y; w[4 * q + 2] = u.z; w[4 * q + 3] = u.w;
+        }
+#pragma unroll
+        for (int k = 0; k < NW; k++) d[k] = w[half * NW + k];
+      }
+    } else {  // packed: PACKED_WORDS words = PACKED_WORDS / 4 pieces per coordinate
+      constexpr int PQ = F::PACKED_WORDS / 4;
+      uint32_t w[F::PACKED_WORDS];
+#pragma unroll
+      for (int q = 0; q < PQ; q++) {
+        const uint4 u = pre[half * PQ + q][lane];
+        w[4 * q] = u.x; w[4 * q + 1] = u.y; w[4 * q + 2] = u.z; w[4 * q + 3] = u.w;
+      }
+      v = F::unpack(w);
+    }
+    return v;
+  };
+  // y of base j (negated for a negative digit), then base j+1's prefetch into the same slot
+  auto take_y = [&](uint32_t j) {
+    T y = base_coord(1);
+    if (e_cur & 0x80000000u) y = F::template sub<1>(F::zero(), y);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
+    if (j + 1 < end) {
+      issue(e_next);
+      e_cur = e_next;
+      e_next = (j + 2 < end) ? (entries ? entries[j + 2] : j + 2) : 0u;
+    }
+    return y;
+  };
+  T X = F::zero(), Y = F::zero();
+  bool ident = true;
+  auto flush = [&](XYZZ<F>* dst) {
+    XYZZ<F> p;
+    if (ident) {
+      p = Cv::identity();
+    } else {
+      p.X = X; p.Y = Y; p.ZZ = get_zz(); p.ZZZ = get_rows(zzz_s);
+    }
+    store_point<Cv>(dst, p);
+  };
+  for (uint32_t j = start; j < end; j++) {
+    if (j == next) {
+      flush(started_here ? &bucket_sums[b] : &conts[seg]);
+      b++;
+      while (offsets[b + 1] <= j) b++;
+      next = offsets[b + 1];
+      started_here = true;
+      ident = true;
+    }
+    __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
+    const T x2 = base_coord(0);
+    // (a batch-affine level record of the point at infinity: word 13 of x, limbs only)
+    if (limbs && (reinterpret_cast<const uint32_t*>(&x2)[13] & AFF_IDENT)) {
+      (void)take_y(j);
+      continue;
+    }
+    if (ident) {
+      Y = take_y(j);
+      X = x2;
+      put_zz(F::one());
+      put_rows(zzz_s, F::one());
+      ident = false;
+      continue;
+    }
+    // (scheduling barriers between the products: interleaving two Fp2 products' working sets
+    // is what overflows the register file)
+    const T ZZ1 = get_zz();
+    T Pd = F::template sub<Cv::KX>(F::mul(x2, ZZ1), X);  // U2 - X1 < 18p
+    G2_SB();
+    const T y2 = take_y(j);
+    T R = F::template sub<Cv::KY>(F::mul(y2, get_rows(zzz_s)), Y);  // S2 - Y1 < 6p
+    G2_SB();
+    // P = +-a (rare): P == -a gives the identity; P == a takes this instruction stream as
+    // dbl-2008-s of P (Pd := 2 Y1 < 8p, R := 3 X1^2 < 6p, no PPP term in X3), as G1's unified madd
+    bool twice = false, neg = false;
+    if (F::is_zero(Pd)) {
+      twice = F::is_zero(R);
+      neg = !twice;
+      if (twice) {
+        Pd = F::add(Y, Y);
+        const T xx = F::sqr(X);
+        R = F::add(F::add(xx, xx), xx);
+      }
+    }
+    G2_SB();
+    const T PP = F::sqr(Pd);
+    G2_SB();
+    put_zz(F::mul(ZZ1, PP));  // ZZ3
+    G2_SB();
+    const T PPP = F::mul(Pd, PP);
+    G2_SB();
+    put_rows(zzz_s, F::mul(get_rows(zzz_s), PPP));  // ZZZ3
+    G2_SB();
+    const T Q = F::mul(X, PP);
+    G2_SB();
+    const T Q2 = F::add(Q, Q);
+    const T X3 = F::template sub<Cv::K1>(F::sqr(R), twice ? Q2 : F::add(PPP, Q2));
+    G2_SB();
+    if constexpr (std::is_same<F, Fp2Ops>::value) {  // (two products: one at a time)
+      const T RQ3 = F::mul(R, F::template sub<Cv::K2>(Q, X3));
+      G2_SB();
+      Y = F::template sub<2>(RQ3, F::mul(Y, PPP));  // < 4p
+    } else {  // one reduction for both products (fe_mul2)
+      Y = F::template mul_sub<Cv::KY>(R, F::template sub<Cv::K2>(Q, X3), Y, PPP);
+    }
+    X = X3;
+    if (neg) ident = true;
+    G2_SB();
+  }
+  flush(started_here ? &bucket_sums[b] : &conts[seg]);
+}
+
 // Bucket accumulation: thread `seg` adds the bases of sorted entries [seg*S, seg*S + S) into
 // their buckets (XYZZ mixed additions), storing a bucket's sum when the bucket ends inside the
 // segment, or its continuation partial (conts[seg]) when the bucket started in an earlier
@@ -432,11 +626,11 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   constexpr bool G1 = std::is_same<C, G1Ops>::value;
   constexpr int NW = sizeof(typename F::T) / 4;    // raw limb words per coordinate (G1: 14)
   constexpr int NQ = NW / 2;                       // 16-byte pieces per raw-limb base (G1 7, G2 14)
-  // G1 window-table records hold raw limbs (G1_TABLE_REC, 7 pieces, no unpacking), and so do the
+  // Window-table records hold raw limbs (G1_TABLE_REC 7 pieces, G2_TABLE_REC 14: no unpacking), and so do the
   // batch-affine levels' records (G1_AFF_REC / G2_AFF_REC: read in order, entries == null; a
-  // record of the point at infinity, AFF_IDENT in word 13, is skipped); plain vectors and G2
-  // tables are packed (6 / 12 pieces)
-  const bool limbs = G1 ? (rec == G1_TABLE_REC || rec == G1_AFF_REC) : rec == G2_AFF_REC;
+  // record of the point at infinity, AFF_IDENT in word 13, is skipped); plain vectors are packed
+  // (6 / 12 pieces)
+  const bool limbs = G1 ? (rec == G1_TABLE_REC || rec == G1_AFF_REC) : (rec == G2_TABLE_REC || rec == G2_AFF_REC);
   const int nq = limbs ? NQ : 2 * PW / 4;
   __shared__ uint4 pre[4][NQ][64];
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
@@ -462,6 +656,20 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
   if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
+#ifndef BH_G2_ACC_REGS
+  if constexpr (!G1) {
+    accumulate_lds<F, NW, NQ, true>(pre[wv], lane, nq, limbs, entries, offsets, start, end, pos0, seg, b, next,
+                                    started_here, e_cur, e_next, issue, bucket_sums, conts);
+    return;
+  }
+#endif
+#ifdef BH_G1_ACC_LDS  // (A/B) G1 through the same loop: ZZZ in LDS (BH_G1_ACC_LDS=2: ZZ too)
+  if constexpr (G1) {
+    accumulate_lds<F, NW, NQ, BH_G1_ACC_LDS == 2>(pre[wv], lane, nq, limbs, entries, offsets, start, end, pos0, seg,
+                                                  b, next, started_here, e_cur, e_next, issue, bucket_sums, conts);
+    return;
+  }
+#endif
   typename C::P acc = C::identity();
   for (uint32_t j = start; j < end; j++) {
     if (j == next) {

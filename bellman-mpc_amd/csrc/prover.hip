@@ -332,7 +332,7 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
   const int W = (256 + c - 1) / c;
   if ((unsigned __int128)hi * W >= ((size_t)1 << 31)) return BH_OK;  // entry encoding limit (global index)
   const bool g2 = srs->group == BH_G2;
-  const uint32_t rec = g2 ? 64 : G1_TABLE_REC;  // 192-byte packed / 112-byte raw-limb points in whole 128-byte lines
+  const uint32_t rec = g2 ? G2_TABLE_REC : G1_TABLE_REC;  // 224 / 112-byte raw-limb points in whole 128-byte lines
   const size_t n = hi - lo;
   const size_t bytes = n * W * rec * 4;
   const size_t chunk = std::min<size_t>(n, (size_t)1 << 19);
