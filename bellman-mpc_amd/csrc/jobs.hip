@@ -23,6 +23,7 @@ using namespace bh;
 struct bh_job_slot {
   hipEvent_t uploaded = nullptr, sorted = nullptr, accumulated = nullptr, done = nullptr;
   uint64_t use = 0;  // bumped each time the slot is taken (bh_job_registry::SortRec validity)
+  uint64_t last_key = 0;  // job_key() of the last multiexp this slot ran (take_slot's match)
   DevBuf raw, scalars, dwords, idx, dtmp, dscan, dscan2, dspan;
   MsmWorkspace<G1Ops> ws1;
   MsmWorkspace<G2Ops> ws2;
@@ -52,17 +53,33 @@ struct bh_job {
 
 namespace {
 
-bh_status take_slot(bh_job_registry& reg, bh_job_slot** out) {
+// The shape of a multiexp for slot reuse: a slot whose buffers were sized by the same kind of
+// job (same bases, offset, length) needs no reallocation -- and a reallocation is a hipFree, which
+// waits for the whole device (the submit would block behind every multiexp in flight).
+uint64_t job_key(const bh_srs* bases, size_t base_offset, size_t n) {
+  uint64_t h = (uint64_t)(uintptr_t)bases * 0x9e3779b97f4a7c15ull;
+  h ^= (base_offset + 0x632be59bd9b4e019ull) + (h << 6) + (h >> 2);
+  h ^= (n + 0x85ebca77c2b2ae63ull) + (h << 6) + (h >> 2);
+  return h | 1u;
+}
+
+bh_status take_slot(bh_job_registry& reg, bh_job_slot** out, uint64_t key) {
   {
     std::lock_guard<std::mutex> lk(reg.mu);
     if (!reg.free_slots.empty()) {
-      *out = reg.free_slots.back();
-      reg.free_slots.pop_back();
+      // the slot that last ran this kind of job, else the most recently freed one
+      auto it = std::find_if(reg.free_slots.rbegin(), reg.free_slots.rend(),
+                             [key](const bh_job_slot* sl) { return sl->last_key == key; });
+      auto pos = it != reg.free_slots.rend() ? std::next(it).base() : std::prev(reg.free_slots.end());
+      *out = *pos;
+      reg.free_slots.erase(pos);
       (*out)->use++;
+      (*out)->last_key = key;
       return BH_OK;
     }
   }
   std::unique_ptr<bh_job_slot> s(new bh_job_slot());
+  s->last_key = key;
   for (hipEvent_t* e : {&s->uploaded, &s->sorted, &s->accumulated, &s->done})
     BH_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   *out = s.release();
@@ -333,7 +350,7 @@ bh_status bh_multiexp_submit(bh_ctx* ctx, const bh_srs* bases, size_t base_offse
     *out = job.release();
     return BH_OK;
   }
-  if ((s = take_slot(*job->reg, &job->slot))) return s;
+  if ((s = take_slot(*job->reg, &job->slot, job_key(bases, base_offset, n)))) return s;
   bh_job_slot* sl = job->slot;
   // the caller's buffers are read before submit returns (pageable copies complete on return)
   bool ok = !sl->raw.alloc(n * 32) && !sl->scalars.alloc(n * 32);
@@ -382,7 +399,7 @@ bh_status bh_multiexp_submit_scalars(bh_ctx* ctx, const bh_srs* bases, size_t ba
     *out = job.release();
     return BH_OK;
   }
-  if ((s = take_slot(*job->reg, &job->slot))) return s;
+  if ((s = take_slot(*job->reg, &job->slot, job_key(bases, base_offset, n)))) return s;
   job->scalars_hold = exps->buf;
   bh_scalar_buf* buf = exps->buf.get();
   const uint32_t* d_sc = buf->d.as<uint32_t>();

@@ -429,12 +429,16 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const t
 #else
 #define G2_SB()
 #endif
-template <class F, int NW, int NQ, bool ZZ_LDS, class Issue>
+// DIRECT: no LDS prefetch slots (pre unused): each coordinate of the base is loaded from `bases`
+// when it is needed, and the other wave of the SIMD covers the latency (two waves per SIMD: 57 KB
+// of LDS per 256-thread block instead of 114).
+template <class F, int NW, int NQ, bool ZZ_LDS, bool DIRECT = false, class Issue>
 __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int nq, bool limbs,
                                                const uint32_t* entries, const uint32_t* offsets, uint32_t start,
                                                uint32_t end, uint32_t pos0, uint32_t seg, uint32_t b, uint32_t next,
                                                bool started_here, uint32_t e_cur, uint32_t e_next, Issue& issue,
-                                               XYZZ<F>* bucket_sums, XYZZ<F>* conts) {
+                                               XYZZ<F>* bucket_sums, XYZZ<F>* conts,
+                                               const uint32_t* bases = nullptr, uint32_t rec = 0) {
   using T = typename F::T;
   using Cv = CurveOps<F>;
   // rows of VW-word vectors, one column per thread: uint4 rows for G2 (7 per coordinate), uint2
@@ -481,6 +485,27 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
   // coordinate `half` (0 = x, 1 = y) of the base in this lane's prefetch slot
   auto base_coord = [&](int half) {
     T v;
+    if constexpr (DIRECT) {
+      const uint4* src = reinterpret_cast<const uint4*>(bases + (size_t)(e_cur & 0x7fffffffu) * rec);
+      uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+      if (limbs) {
+#pragma unroll
+        for (int q = 0; q < NW / 4; q++) {
+          const uint4 u = src[half * (NW / 4) + q];
+          d[4 * q] = u.x; d[4 * q + 1] = u.y; d[4 * q + 2] = u.z; d[4 * q + 3] = u.w;
+        }
+      } else {
+        constexpr int PQ = F::PACKED_WORDS / 4;
+        uint32_t w[F::PACKED_WORDS];
+#pragma unroll
+        for (int q = 0; q < PQ; q++) {
+          const uint4 u = src[half * PQ + q];
+          w[4 * q] = u.x; w[4 * q + 1] = u.y; w[4 * q + 2] = u.z; w[4 * q + 3] = u.w;
+        }
+        v = F::unpack(w);
+      }
+      return v;
+    }
     if (limbs) {  // raw limbs: words [half*NW, half*NW + NW) of the record
       uint32_t* d = reinterpret_cast<uint32_t*>(&v);
       if constexpr (NW % 4 == 0) {  // G2: pieces [half*NW/4, half*NW/4 + NW/4)
@@ -516,9 +541,9 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
   auto take_y = [&](uint32_t j) {
     T y = base_coord(1);
     if (e_cur & 0x80000000u) y = F::template sub<1>(F::zero(), y);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
+    if constexpr (!DIRECT) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
     if (j + 1 < end) {
-      issue(e_next);
+      if constexpr (!DIRECT) issue(e_next);
       e_cur = e_next;
       e_next = (j + 2 < end) ? (entries ? entries[j + 2] : j + 2) : 0u;
     }
@@ -544,7 +569,7 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
       started_here = true;
       ident = true;
     }
-    __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
+    if constexpr (!DIRECT) __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
     const T x2 = base_coord(0);
     // (a batch-affine level record of the point at infinity: word 13 of x, limbs only)
     if (limbs && (reinterpret_cast<const uint32_t*>(&x2)[13] & AFF_IDENT)) {
@@ -715,9 +740,53 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   else store_point<C>(&conts[seg], acc);
 }
 
+// G2 accumulation without LDS prefetch slots (accumulate_lds<DIRECT>): 57 KB of LDS per block and
+// at most 256 registers, so two waves per SIMD.  Same segments, bookkeeping and results as
+// k_accumulate_pf<G2> (BH_G2_DIRECT=1 selects it: A/B).
+template <class C>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_accumulate_g2d(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt, const uint32_t* bases, uint32_t rec,
+                 uint32_t S, uint32_t b_lo, uint32_t b_hi, typename C::P* bucket_sums, typename C::P* conts,
+                 uint32_t* cont_bucket) {
+  using F = Fp2Ops;
+  constexpr int NW = sizeof(typename F::T) / 4;
+  const bool limbs = rec == G2_TABLE_REC || rec == G2_AFF_REC;
+  const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
+  const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t pos0 = seg * S;
+  const uint32_t start = max(pos0, E_lo);
+  if (pos0 >= E_hi || start >= pos0 + S) return;
+  const uint32_t end = min(pos0 + S, E_hi);
+  auto entry = [&](uint32_t j) { return entries ? entries[j] : j; };
+  const uint32_t e_cur = entry(start);
+  const uint32_t e_next = (start + 1 < end) ? entry(start + 1) : 0u;
+  const uint32_t b = find_bucket(offsets, nbt, start);
+  const uint32_t next = offsets[b + 1];
+  const bool started_here = offsets[b] >= pos0;
+  if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
+  auto no_issue = [](uint32_t) {};
+  accumulate_lds<F, NW, NW / 2, true, true>(nullptr, 0, 0, limbs, entries, offsets, start, end, pos0, seg, b, next,
+                                           started_here, e_cur, e_next, no_issue, bucket_sums, conts, bases, rec);
+}
+
 // Segment length S so that the accumulation grid is exactly ROUNDS full waves of
 // resident workgroups (occupancy from the compiled kernel, CUs from the device): a
 // partial last round would leave most of the chip idle for its whole duration.
+// BH_G2_DIRECT=1 (A/B): the G2 accumulation without LDS prefetch slots, two waves per SIMD
+inline bool g2_direct() {
+  static const bool v = [] {
+    const char* e = getenv("BH_G2_DIRECT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+template <class C>
+const void* accumulate_kernel() {
+  if constexpr (!std::is_same<C, G1Ops>::value)
+    if (g2_direct()) return (const void*)k_accumulate_g2d<C>;
+  return (const void*)k_accumulate_pf<C>;
+}
+
 template <class C>
 void fit_segments_E(MsmShape& sh, size_t E);
 template <class C>
@@ -730,7 +799,7 @@ void fit_segments_E(MsmShape& sh, size_t E) {
     int dev = 0, cus = 256, blocks = 1;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const void* k = (const void*)k_accumulate_pf<C>;
+    const void* k = accumulate_kernel<C>();
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
     return (size_t)cus * (size_t)blocks * 256;
   }();
@@ -948,14 +1017,23 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
       }
     }
     const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
-    hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                       ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, 0u, cut, ws.bucket_sums, ws.conts,
-                       ws.cont_bucket);
+    auto launch = [&](uint32_t lo, uint32_t hi) {
+      if constexpr (!std::is_same<C, G1Ops>::value) {
+        if (g2_direct()) {
+          hipLaunchKernelGGL(k_accumulate_g2d<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                             ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, lo, hi, ws.bucket_sums,
+                             ws.conts, ws.cont_bucket);
+          return;
+        }
+      }
+      hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
+                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, lo, hi, ws.bucket_sums, ws.conts,
+                         ws.cont_bucket);
+    };
+    launch(0u, cut);
     if (sh.halves) {
       if (timing && timing->ev_half) hipEventRecord(timing->ev_half, st);
-      hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(segs, 256)), dim3(256), 0, st, ws.entries,
-                         ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, cut, (uint32_t)nbt, ws.bucket_sums,
-                         ws.conts, ws.cont_bucket);
+      launch(cut, (uint32_t)nbt);
     }
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
   }
@@ -1085,6 +1163,8 @@ template <class C>
 void msm_acc_kernels(std::vector<KernInfo>& v) {
   v.push_back({std::is_same<C, G1Ops>::value ? "k_accumulate_pf<G1>" : "k_accumulate_pf<G2>",
                (const void*)k_accumulate_pf<C>, 256, 0});
+  if constexpr (!std::is_same<C, G1Ops>::value)
+    v.push_back({"k_accumulate_g2d", (const void*)k_accumulate_g2d<C>, 256, 0});
 }
 template <class C>
 void msm_back_kernels(std::vector<KernInfo>& v) {

@@ -1073,9 +1073,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (last_rounds > 0 && last_rounds < 4) sl.S = std::min(sl.S * 4 / last_rounds, 1 << 16);
   }
   // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it;
-  // 1 = from the start, concurrent with everything; 2 = after the first accumulation (the
-  // replicated default: H's ~4.5 ms of NTT work fills the later accumulations' round
-  // boundaries and is done before h, accumulated last; ~1 ms faster than 1 at 2^22).
+  // 1 = from the start, concurrent with everything (the default); 2 = after the first
+  // accumulation (round 3's replicated default, when the first accumulation -- b_g2_aux --
+  // took a SIMD's whole register file and H's passes could not share its SIMDs).  Since the G2
+  // accumulation keeps ZZ/ZZZ in LDS (268 registers, msm_impl.cuh accumulate_lds), H's NTT passes
+  // co-reside with it: same-box A/B at 2^22, 55.1-55.3 ms per proof with 1 against 57.4-58.2 with
+  // 2 (3: 55.7-56.2; profiles/r04_ab_hmode_g2.txt).
   static const int h_mode_env = [] {
     const char* e = getenv("BH_H_MODE");
     return e ? atoi(e) : -1;
@@ -1086,7 +1089,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
   // thread 10.44, and H held until the first sorts are done 10.61-10.73 against 10.28-10.37 (neither
   // kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
-  int h_mode = h_mode_env >= 0 ? h_mode_env : (dh != nullptr ? 1 : 2);
+  int h_mode = h_mode_env >= 0 ? h_mode_env : 1;
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
