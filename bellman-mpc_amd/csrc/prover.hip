@@ -1089,7 +1089,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
   // thread 10.44, and H held until the first sorts are done 10.61-10.73 against 10.28-10.37 (neither
   // kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
-  int h_mode = h_mode_env >= 0 ? h_mode_env : 1;
+  // (from host buffers, bh_prove: 2 -- enqueue_h waits on the host until a, b, c are staged, and
+  // placed first that wait would hold back every other enqueue: 68.4 against 56.5 ms resident)
+  int h_mode = h_mode_env >= 0 ? h_mode_env : (up ? 2 : 1);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
