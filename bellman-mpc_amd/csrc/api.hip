@@ -1190,6 +1190,14 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
       BH_TRY_HIP(bg.abc.alloc(3 * m * 32));  // stream order on bg.st protects it across producers
       uint32_t* abc = bg.abc.as<uint32_t>();
       const uint64_t* src[3] = {a, b, c};
+      // BH_HOST_TIMING: the producer's stages on stderr (ms since the call)
+      static const bool timing = getenv("BH_HOST_TIMING") != nullptr;
+      const auto t0 = std::chrono::steady_clock::now();
+      auto stamp = [&](const char* what, int v) {
+        if (timing)
+          fprintf(stderr, "h producer: %s %d at %.2f ms\n", what, v,
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+      };
       for (int v = 0; v < 3; v++) {
         uint32_t* dst = abc + (size_t)v * m * 8;
         if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.st));
@@ -1203,9 +1211,11 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
                                     reinterpret_cast<const uint8_t*>(src[v]) + off, std::min(piece, nc * 32 - off),
                                     bg.st));
           }
+          stamp("uploaded", v);
           launch_fr_convert(dst, dst, nc, fr_to_dev_const(), 0, bg.st);
         }
       }
+      stamp("enqueueing H", 3);
       // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
       bh_status hs = run_h_pipeline(ctx, D, abc, bg.st, nullptr, raw->d.as<uint32_t>());
       if (hs) return hs;
