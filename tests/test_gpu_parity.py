@@ -950,3 +950,61 @@ def test_shared_sorts_follow_the_vector_not_its_address(ctx):
         assert got == (bh.multiexp(ctx, Lv, 0, None, ex, montgomery=True),
                        bh.multiexp(ctx, B1, off, dens, ex, montgomery=True),
                        bh.multiexp(ctx, B2, off, dens, ex, montgomery=True))
+
+
+_G2_DIRECT_SCRIPT = r"""
+import json, os, random, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "bellman-mpc_amd"))
+sys.path.insert(0, sys.argv[1])
+import bellman_hip as bh
+from oracle import bellman as bm
+from oracle import bls12_381 as bls
+R = %d
+ctx = bh.Context(0)
+E = bm.BLS12_381
+aff = lambda k: E.G2.to_affine(E.G2.mul(bls.G2.generator(), k %% R))
+rng = random.Random(21)
+pts = [aff(11)] * 24 + [aff(R - 11)] * 24 + [aff(29)] * 16 + [aff(rng.randrange(1, R)) for _ in range(8)]
+bases = bh.Bases(ctx, bh.BH_G2, b"".join(bls.g2_to_uncompressed(p) for p in pts))
+e1, e2 = rng.randrange(R), rng.randrange(R)
+cases = [[e1] * 48 + [e2] * 16 + [rng.randrange(R) for _ in range(8)], [1] * 24 + [R - 1] * 24 + [2] * 16 + [0] * 8]
+msm = [bh.multiexp(ctx, bases, 0, None, ex).hex() for ex in cases]
+rounds = (1 << 16) - 1
+params = bh.Parameters.chain(ctx, rounds)
+w = bh.Witness.chain(ctx, rounds)
+params.prepare(w)
+proof = bh.prove_witness(ctx, params, w, 27134, 17146).hex()
+print(json.dumps({"cases": [[str(x) for x in ex] for ex in cases], "msm": msm, "proof": proof}))
+""" % R
+
+
+def test_g2_direct_accumulation_equals_default(ctx):
+    """The direct-load G2 accumulation (BH_G2_DIRECT=1: no LDS prefetch slots, two waves per SIMD;
+    msm_impl.cuh k_accumulate_g2d) in a process of its own: G2 multiexps with equal and opposite bases
+    in one bucket equal the oracle, and a 2^17-constraint proof over window tables (its b_g2_aux
+    accumulation is the G2 kernel) equals this process's proof on the default kernel."""
+    import json
+    import os
+    import subprocess
+    import sys
+    bh = _bh()
+    from oracle import bellman as bm
+    from oracle import bls12_381 as bls
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, BH_G2_DIRECT="1")
+    p = subprocess.run([sys.executable, "-c", _G2_DIRECT_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    E = bm.BLS12_381
+    aff = lambda k: E.G2.to_affine(E.G2.mul(bls.G2.generator(), k % R))
+    rng = random.Random(21)
+    pts = [aff(11)] * 24 + [aff(R - 11)] * 24 + [aff(29)] * 16 + [aff(rng.randrange(1, R)) for _ in range(8)]
+    for ex, m in zip(got["cases"], got["msm"]):
+        want = bls.g2_to_uncompressed(E.G2.to_affine(bm.multiexp(E, E.G2, pts, 0, None, [int(x) for x in ex])))
+        assert bytes.fromhex(m) == want
+    rounds = (1 << 16) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    params.prepare(w)
+    assert bh.prove_witness(ctx, params, w, 27134, 17146).hex() == got["proof"]
