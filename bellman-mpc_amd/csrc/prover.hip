@@ -1089,9 +1089,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
   // thread 10.44, and H held until the first sorts are done 10.61-10.73 against 10.28-10.37 (neither
   // kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
-  // (from host buffers, bh_prove: 2 -- enqueue_h waits on the host until a, b, c are staged, and
-  // placed first that wait would hold back every other enqueue: 68.4 against 56.5 ms resident)
-  int h_mode = h_mode_env >= 0 ? h_mode_env : (up ? 2 : 1);
+  // 5 = enqueued right before h's own sort and accumulation, after every other sort and
+  // accumulation: the default from host buffers (bh_prove), where enqueue_h first waits on the host
+  // until a, b, c are staged -- placed first (mode 1) that wait held back every other enqueue (68.4
+  // against 56.5 ms resident); placed last, the device is busy with the queued accumulations
+  // meanwhile, and H still starts as soon as its upload lands, beside the first accumulation.
+  int h_mode = h_mode_env >= 0 ? h_mode_env : (up ? 5 : 1);
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -1155,12 +1158,22 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
   if (h_mode == 3 && (s = enqueue_h(jev[33]))) return s;
   const auto t_h = std::chrono::steady_clock::now();
+  const bool h_late = h_mode == 5;
   for (int r = pre_sorts; r < ns; r++) {
+    if (h_late && jobs[sorder[r]].is_h) continue;  // behind H, enqueued below
     if ((s = sort_h_or(sorder[r]))) return s;
   }
   const auto t_sorts = std::chrono::steady_clock::now();
-  for (int q = 1; q < nbig; q++)
+  bool h_done = !h_late;
+  for (int q = 1; q < nbig; q++) {
+    if (!h_done && jobs[big[q]].is_h) {
+      if ((s = enqueue_h(jev[33]))) return s;
+      if ((s = sort_h_or(big[q]))) return s;
+      h_done = true;
+    }
     if ((s = acc_job(big[q], sA))) return s;
+  }
+  if (!h_done && (s = enqueue_h(jev[33]))) return s;  // (no large h job: H still runs)
   if (nbig > 0) last_acc = big[nbig - 1];
   if ((s = run_small())) return s;
   // The host waits below are on events of THIS proof's work (not stream syncs): on a pipelined
