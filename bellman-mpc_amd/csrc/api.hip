@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
 #include <chrono>
 #include <thread>
 
@@ -1107,13 +1109,57 @@ bh_status bh_params_vector(const bh_params* p, int which, const bh_srs** out) {
   }
 }
 
+namespace {
+struct ScalarPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> bufs;  // bytes -> device pointer
+  size_t held = 0;
+};
+ScalarPool g_scalar_pool[64];
+constexpr size_t SCALAR_POOL_CAP = (size_t)2 << 30;  // per device
+}  // namespace
+
+void* scalar_pool_take(int device, size_t bytes, size_t* got) {
+  if (device < 0 || device >= 64) return nullptr;
+  ScalarPool& pl = g_scalar_pool[device];
+  std::lock_guard<std::mutex> lk(pl.mu);
+  auto it = pl.bufs.lower_bound(bytes);
+  if (it == pl.bufs.end() || it->first > bytes + bytes / 4) return nullptr;  // (no gross over-size)
+  void* p = it->second;
+  *got = it->first;
+  pl.held -= it->first;
+  pl.bufs.erase(it);
+  return p;
+}
+
+void scalar_pool_give(int device, void* p, size_t bytes) {
+  if (device >= 0 && device < 64) {
+    ScalarPool& pl = g_scalar_pool[device];
+    std::lock_guard<std::mutex> lk(pl.mu);
+    if (pl.held + bytes <= SCALAR_POOL_CAP) {
+      pl.bufs.emplace(bytes, p);
+      pl.held += bytes;
+      return;
+    }
+  }
+  (void)hipSetDevice(device);
+  (void)hipFree(p);
+}
+
 static bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out) {
   static std::atomic<uint64_t> next_id{1};
   auto buf = std::make_shared<bh_scalar_buf>();
   buf->device = ctx->device;
   buf->owner = ctx;
   buf->id = next_id.fetch_add(1);
-  BH_TRY_HIP(buf->d.alloc(std::max<size_t>(n, 1) * 32));
+  const size_t bytes = std::max<size_t>(n, 1) * 32;
+  size_t got = 0;
+  if (void* p = scalar_pool_take(ctx->device, bytes, &got)) {
+    buf->d.p = p;
+    buf->d.bytes = got;
+  } else {
+    BH_TRY_HIP(buf->d.alloc(bytes));
+  }
   BH_TRY_HIP(hipEventCreateWithFlags(&buf->ready, hipEventDisableTiming));
   *out = std::move(buf);
   return BH_OK;

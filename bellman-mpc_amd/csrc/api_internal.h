@@ -157,6 +157,13 @@ constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use pla
 // passes): until that thread has enqueued its work (`enqueued`), `ready` is not recorded yet, so
 // multiexps submitted meanwhile park their own enqueue in `deferred`, which the producer runs,
 // under mu, right after recording `ready` (argument: the producer's status).
+// Device buffers of finished scalar vectors, kept per device for the next vector of the same size
+// (api.hip): a vector's hipFree would wait for the whole device, and a caller that drops one while
+// another proof's multiexps run (a seam caller's Arcs) would hold every HIP call of the process
+// behind them.  take: a buffer of at least `bytes` or null; give: keeps it (bounded) or frees it.
+extern "C" void* scalar_pool_take(int device, size_t bytes, size_t* got);
+extern "C" void scalar_pool_give(int device, void* p, size_t bytes);
+
 struct bh_scalar_buf {
   bh::DevBuf d;
   uint64_t id = 0;  // unique per vector (jobs' sort sharing is keyed on it, not on d's address)
@@ -182,6 +189,10 @@ struct bh_scalar_buf {
       (void)hipEventSynchronize(ready);
       (void)hipEventDestroy(ready);
     }
+    // (every multiexp that read it has been waited for: the jobs hold this buffer until then)
+    if (d.p) scalar_pool_give(device, d.p, d.bytes);
+    d.p = nullptr;
+    d.bytes = 0;
   }
 };
 struct bh_scalars {
