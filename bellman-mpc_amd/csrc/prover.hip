@@ -1151,8 +1151,17 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     int wait_j = big[0];
     for (int r = 0; r < pre_sorts; r++)
       if (sorted_from[sorder[r]] == sorder[r]) wait_j = sorder[r];
-    BH_TRY_HIP(hipStreamWaitEvent(sA, jev[16 + wait_j], 0));
-    if ((s = acc_job(big[0], sA))) return s;
+    // The first accumulation (G2: 268 registers, one wave per SIMD) runs on the small-multiexp
+    // stream (idle when the public-input multiexps are on the host), so the G1 accumulations start
+    // beside it instead of after it: same-box A/B at 2^22 54.66-55.17 against 55.01-55.45 ms
+    // (profiles/r04_ab_first_acc_stream.txt).  BH_FIRST_ACC_STREAM=0: on the main stream.
+    static const bool first_own = [] {
+      const char* e = getenv("BH_FIRST_ACC_STREAM");
+      return !(e && e[0] == '0');
+    }();
+    hipStream_t s0 = (first_own && nsmall == 0 && !serial) ? sT : sA;
+    BH_TRY_HIP(hipStreamWaitEvent(s0, jev[16 + wait_j], 0));
+    if ((s = acc_job(big[0], s0))) return s;
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
