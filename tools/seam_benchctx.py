@@ -31,4 +31,6 @@ for _ in range(10):
     t0 = time.perf_counter()
     bh.prove_seam(ctx, params, asg, r, s)
     ts.append(round((time.perf_counter() - t0) * 1e3, 2))
+    if os.environ.get("BH_HOST_TIMING"):
+        print(f"call {len(ts)}: {ts[-1]} ms", file=sys.stderr, flush=True)
 print(mode, ts, "mean of the last 8", round(sum(ts[2:]) / 8, 2), flush=True)
