@@ -30,12 +30,12 @@ sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point, scalar)
 G2_PAIR_BYTES = 224
-TRAFFIC_FILE = "r04_pmc_traffic_accumulate_g1.json"  # tools/pmc_traffic.py output for the 2^22 workload
+TRAFFIC_FILE = "r05_pmc_traffic_accumulate_g1.json"  # tools/pmc_round.py output for the 2^22 workload
 G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X (profiles/r01_curvebench.txt)
 G1_MADD_PEAK_CLOCK_GHZ = 2.27  # the clock curvebench's G1 (2 waves) kernel held (profiles/r03_curvebench_clock.txt)
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
-PMC_FILE = "r04_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_report.py over the 2^22 bench (+ held clocks)
+PMC_FILE = "r05_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_round.py over the 2^22 bench (+ held clocks, trace)
 SOLO_WAVE_INSTR_RATE = 510.0   # G wave-instr/s: the G1 accumulation alone (6.38 G madd/s x 5116 lane-instr / 64;
                                # profiles/r03_ab_accumulate_variants.txt serial run, r03_pmc_2p22.json)
 
@@ -343,13 +343,33 @@ def main():
         with open(tpath) as f:
             traffic = round(json.load(f)["traffic_bytes_per_launch"])
         traffic_src = f"profiles/{TRAFFIC_FILE} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate passes)"
+    alg_per_launch = pairs * G1_PAIR_BYTES / launches if launches else None
     roof = {"bound": "hbm", "kernel": "k_accumulate_pf<G1>",
             "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": traffic,
             "traffic_source": traffic_src,
             "avg_launch_ms": round(acc_ms / launches, 4) if launches else None,
-            "algorithmic_bytes_per_launch": round(pairs * G1_PAIR_BYTES / launches) if launches else None,
+            "avg_launch_source": "HIP events around every launch of the timed steps, on the stream it runs on; "
+                                 "the launches co-run with the G2 accumulation and H as shipped",
+            "algorithmic_bytes_per_launch": round(alg_per_launch) if launches else None,
             "note": "VALU-bound (XYZZ mixed additions on 29-bit limbs): see DESIGN.md section 4"}
+    # the same kernel in the committed profiles of this workload: its rocprofv3 kernel-trace average
+    # (same co-running schedule; must agree with avg_launch_ms) and its solo duration in the counter
+    # passes (rocprofv3 --pmc serialises dispatches)
+    ppath = os.path.join(ROOT, "profiles", PMC_FILE)
+    if os.path.exists(ppath) and k == 22 and launches:
+        with open(ppath) as f:
+            pmc = json.load(f)
+        tr = pmc.get("trace_g1_accumulate")
+        if tr:
+            roof["rocprof_avg_launch_ms"] = tr["avg_ms"]
+            roof["rocprof_frac"] = round(alg_per_launch / (tr["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5)
+            roof["rocprof_source"] = f"profiles/{PMC_FILE} trace_g1_accumulate ({tr['source']})"
+            roof["events_vs_rocprof"] = round((acc_ms / launches) / tr["avg_ms"], 4)
+        solo = pmc.get("k_accumulate_pf<CurveOps<FpOps", {}).get("avg_dispatch_ms_grbm_pass")
+        if solo:
+            roof["solo_avg_launch_ms"] = solo
+            roof["solo_frac"] = round(alg_per_launch / (solo / 1e3) / 1e9 / HBM_PEAK_GBS, 5)
     # integer-ALU roofline: G1 mixed additions/s against the microbenchmarked peak, and the
     # v_mad_u64_u32 issue rate they imply (see MADS_PER_G1_MADD)
     g1_adds = sum(t[8] for t in timings)
@@ -481,6 +501,7 @@ def main():
                          "g1_accumulate": round(acc_ms / len(timings), 3),
                          "g2_accumulate": round(sum(t[5] for t in timings) / len(timings), 3),
                          "g1_pairs": int(timings[-1][4]), "g2_pairs": int(timings[-1][7]),
+                         "g1_adds": int(timings[-1][8]), "g2_adds": int(timings[-1][9]),
                          "host_wall_prove": round(sum(t[0] for t in timings) / len(timings), 3)},
         "setup_s": {"crs_generation": round(t_params, 2), "witness_synthesis_and_upload": round(t_wit, 2),
                     "srs_window_tables": round(t_tables, 2) if args.tables else None},
