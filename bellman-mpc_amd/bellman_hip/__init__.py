@@ -278,9 +278,10 @@ class Context:
         return list(out)
 
     def last_stats(self):
-        """bh_last_stats: the 10 timing fields, then tables used / large multiexps / table bytes."""
-        out = (ctypes.c_double * 13)()
-        _check(_lib.bh_last_stats(self.h, out, 13))
+        """bh_last_stats: the 10 timing fields, then tables used / large multiexps / table bytes, then
+        (after prove() from host buffers) the upload landing times of aux, a, b, c and H's end, ms."""
+        out = (ctypes.c_double * 18)()
+        _check(_lib.bh_last_stats(self.h, out, 18))
         return list(out)
 
     def scratch_report(self):

@@ -492,7 +492,8 @@ static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const F
 }
 
 void ctx_sync_all(bh_ctx* ctx) {
-  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d, ctx->bg.st})
+  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d, ctx->bg.cst,
+                         ctx->bg.st})
     if (st) (void)hipStreamSynchronize(st);
   for (hipStream_t st : ctx->tstream)
     if (st) (void)hipStreamSynchronize(st);
@@ -629,29 +630,30 @@ static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind
 // untouched, no copy).  Without hout, on return d_abc's first m entries hold the h coefficients
 // in BIT-REVERSED order (device form); with hout, the last pass writes the m-1 canonical h
 // scalars in natural order to hout instead (truncation + to_le_bits fused).
-bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc,
-                         uint32_t* hout) {
+bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v) {
   const int L = D->L;
   const size_t m = (size_t)1 << L;
-  uint32_t* a = d_abc;
-  uint32_t* b = d_abc + m * 8;
-  uint32_t* c = d_abc + 2 * m * 8;
   // prover.rs:214-219: ifft (DIF, omega^-1) with m^-1 * g^i fused = ifft + distribute_powers(g);
   // then fft (DIT, bit-reversed -> natural) = coset_fft; c's storing pass computes
   // (a*b - c) / Z(g) into a (prover.rs:221-225: mul_assign, sub_assign, divide_by_z_on_coset)
-  for (int v = 0; v < 3; v++) {
-    uint32_t* x = d_abc + (size_t)v * m * 8;
-    launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
-               D->lo_bits, st, src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
-    NttEpilogue e;
-    if (v == 2) {
-      e.kind = NttEpilogue::AB_MINUS_C;
-      e.pa = a;
-      e.pb = b;
-      e.k = D->consts.as<uint32_t>() + 9;
-    }
-    launch_ntt(x, L, false, D->lv_fwd.as<uint32_t>(), nullptr, nullptr, 0, st, nullptr, e);
+  uint32_t* x = d_abc + (size_t)v * m * 8;
+  launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
+             D->lo_bits, st, src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
+  NttEpilogue e;
+  if (v == 2) {
+    e.kind = NttEpilogue::AB_MINUS_C;
+    e.pa = d_abc;
+    e.pb = d_abc + m * 8;
+    e.k = D->consts.as<uint32_t>() + 9;
   }
+  launch_ntt(x, L, false, D->lv_fwd.as<uint32_t>(), nullptr, nullptr, 0, st, nullptr, e);
+  BH_TRY_HIP(hipGetLastError());
+  return BH_OK;
+}
+
+bh_status run_h_final(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, uint32_t* hout) {
+  const int L = D->L;
+  const size_t m = (size_t)1 << L;
   // prover.rs:226: icoset_fft = ifft + distribute_powers(g^-1), fused as above (output bit-reversed)
   NttEpilogue e;
   if (hout) {
@@ -659,10 +661,18 @@ bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st
     e.out = hout;
     e.n_out = (uint32_t)(m - 1);
   }
-  launch_ntt(a, L, true, D->lv_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
+  launch_ntt(d_abc, L, true, D->lv_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
              D->lo_bits, st, nullptr, e);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
+}
+
+bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc,
+                         uint32_t* hout) {
+  bh_status s;
+  for (int v = 0; v < 3; v++)
+    if ((s = run_h_vector(ctx, D, d_abc, st, src_abc, v))) return s;
+  return run_h_final(ctx, D, d_abc, st, hout);
 }
 
 }  // namespace bh
@@ -862,8 +872,11 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   }
   ctx_sync_all(ctx);  // nothing may still read the workspaces released below (jobs' too)
   bh_ctx_release_jobs(ctx);
+  ctx->bg.ring.release();  // (waits for its slots' copies on bg.cst)
   if (ctx->bg.st) (void)hipStreamDestroy(ctx->bg.st);
-  ctx->bg.ring.release();
+  if (ctx->bg.cst) (void)hipStreamDestroy(ctx->bg.cst);
+  for (auto& e : ctx->bg.vec)
+    if (e) (void)hipEventDestroy(e);
   ctx->bg.pool.reset();
   ctx->bg.abc.release();
   if (ctx->h2d) (void)hipStreamSynchronize(ctx->h2d);
@@ -1230,10 +1243,16 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
         int lo = 0, hi = 0;
         BH_TRY_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         BH_TRY_HIP(hipStreamCreateWithPriority(&bg.st, hipStreamNonBlocking, hi));
+        BH_TRY_HIP(hipStreamCreateWithFlags(&bg.cst, hipStreamNonBlocking));
+        for (auto& e : bg.vec) BH_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         BH_TRY_HIP(bg.ring.init());
         bg.pool.reset(new HostPool(3));
       }
-      BH_TRY_HIP(bg.abc.alloc(3 * m * 32));  // stream order on bg.st protects it across producers
+      // a|b|c: the copies (bg.cst) start after the previous producer's H (bg.st) is done with it;
+      // each vector's transforms (bg.st) start as soon as its own copy has landed
+      BH_TRY_HIP(bg.abc.alloc(3 * m * 32));
+      BH_TRY_HIP(hipEventRecord(bg.vec[3], bg.st));
+      BH_TRY_HIP(hipStreamWaitEvent(bg.cst, bg.vec[3], 0));
       uint32_t* abc = bg.abc.as<uint32_t>();
       const uint64_t* src[3] = {a, b, c};
       // BH_HOST_TIMING: the producer's stages on stderr (ms since the call)
@@ -1246,7 +1265,7 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
       };
       for (int v = 0; v < 3; v++) {
         uint32_t* dst = abc + (size_t)v * m * 8;
-        if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.st));
+        if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.cst));
         if (nc) {
           // in 16 MB pieces, paused while a bh_scalars_upload streams (the assignments feed the
           // first sorts; H is needed last)
@@ -1255,15 +1274,19 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
             while (bg.fg_uploads.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
             BH_TRY_HIP(bg.ring.copy(*bg.pool, reinterpret_cast<uint8_t*>(dst) + off,
                                     reinterpret_cast<const uint8_t*>(src[v]) + off, std::min(piece, nc * 32 - off),
-                                    bg.st));
+                                    bg.cst));
           }
           stamp("uploaded", v);
-          launch_fr_convert(dst, dst, nc, fr_to_dev_const(), 0, bg.st);
         }
+        BH_TRY_HIP(hipEventRecord(bg.vec[v], bg.cst));
+        BH_TRY_HIP(hipStreamWaitEvent(bg.st, bg.vec[v], 0));
+        if (nc) launch_fr_convert(dst, dst, nc, fr_to_dev_const(), 0, bg.st);
+        bh_status hs = run_h_vector(ctx, D, abc, bg.st, nullptr, v);
+        if (hs) return hs;
       }
-      stamp("enqueueing H", 3);
+      stamp("H enqueued", 3);
       // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
-      bh_status hs = run_h_pipeline(ctx, D, abc, bg.st, nullptr, raw->d.as<uint32_t>());
+      bh_status hs = run_h_final(ctx, D, abc, bg.st, raw->d.as<uint32_t>());
       if (hs) return hs;
       BH_TRY_HIP(hipEventRecord(raw->ready, bg.st));
       return BH_OK;

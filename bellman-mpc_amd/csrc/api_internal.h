@@ -266,7 +266,7 @@ struct bh_ctx {
   bh::DevBuf hbuf;        // H pipeline scratch (h scalars canonical)
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
-  double last_timings[16] = {};  // bh_last_timings [0,10) + bh_last_stats extras
+  double last_timings[24] = {};  // bh_last_timings [0,10) + bh_last_stats extras
   uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp
   uint32_t* host_spans = nullptr;   // pinned: MAX_SPAN_BLOCKS per-workgroup max_span words per prover multiexp
   bh::DevBuf dspan;                 // device words for max_span (the same layout)
@@ -283,7 +283,9 @@ struct bh_ctx {
   // mu; bh_ctx_destroy waits for bg_active == 0
   struct Background {
     std::mutex mu;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;   // the H transforms
+    hipStream_t cst = nullptr;  // the a, b, c copies
+    hipEvent_t vec[4] = {};     // a, b, c landed; [3] the previous producer's H done
     bh::H2DRing ring;
     std::unique_ptr<bh::HostPool> pool;
     bh::DevBuf abc;
@@ -334,6 +336,10 @@ FrConst fr_to_dev_const();
 bh_status download_fr(bh_ctx* ctx, uint32_t* src, size_t n, uint64_t* host);
 bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc = nullptr,
                          uint32_t* hout = nullptr);
+// the same in stages, so that each vector's transforms can be enqueued as its upload lands:
+// run_h_vector(v) for v = 0, 1, 2 in order (v = 2 folds (a*b - c)/Z into a), then run_h_final
+bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v);
+bh_status run_h_final(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, uint32_t* hout);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,
                          bh_srs* out);
 // reference-exact error semantics of multiexp (EOF / identity), host side

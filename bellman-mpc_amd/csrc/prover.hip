@@ -141,6 +141,18 @@ bh_status witness_host(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint
   return BH_OK;
 }
 
+// Caller (pageable) bytes -> device on the copy stream st.  Default: the pinned staging ring
+// (memcpy workers + DMA).  BH_UPLOAD_DIRECT=1: one hipMemcpyAsync from the pageable buffer (the
+// runtime's own staging; 56 GB/s in tools/microbench/h2dbench.cpp against ~50 for the ring, A/B).
+hipError_t upload_host(bh_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  static const bool direct = [] {
+    const char* e = getenv("BH_UPLOAD_DIRECT");
+    return e && e[0] == '1';
+  }();
+  if (direct) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  return ctx->ring.copy(ctx_pool(ctx), dst, src, bytes, st);
+}
+
 bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint64_t* b, const uint64_t* c,
                               const uint64_t* inputs, const uint64_t* aux, hipStream_t st, UploadSync* up) {
   uint64_t* d = w->dens.as<uint64_t>();
@@ -161,13 +173,19 @@ bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, con
     // prover's own streams convert (compute_msms: aux/inputs before the sorts, a/b/c into
     // the H block's buffer)
     w->raw = true;
-    if (ni) BH_TRY_HIP(ctx->ring.copy(pool, w->inputs.p, inputs, ni * 32, st));
-    if (na) BH_TRY_HIP(ctx->ring.copy(pool, w->aux.p, aux, na * 32, st));
+    if (ni) BH_TRY_HIP(upload_host(ctx, w->inputs.p, inputs, ni * 32, st));
+    if (na) BH_TRY_HIP(upload_host(ctx, w->aux.p, aux, na * 32, st));
     BH_TRY_HIP(hipEventRecord(up->ev[0], st));
     up->set(1);
     const uint64_t* src[3] = {a, b, c};
-    for (int v = 0; v < 3; v++)
-      if (nc) BH_TRY_HIP(ctx->ring.copy(pool, abc + (size_t)v * m * 8, src[v], nc * 32, st));
+    for (int v = 0; v < 3; v++) {
+      if (nc) BH_TRY_HIP(upload_host(ctx, abc + (size_t)v * m * 8, src[v], nc * 32, st));
+      if (up->vec[v]) BH_TRY_HIP(hipEventRecord(up->vec[v], st));
+      if (up->on_vector) {
+        const bh_status hs = (bh_status)up->on_vector(v);
+        if (hs) return hs;
+      }
+    }
     BH_TRY_HIP(hipEventRecord(up->ev[1], st));
     up->set(2);
     return BH_OK;
@@ -639,6 +657,15 @@ bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t n
   return full(&params->b_g2, b_aux_used);
 }
 
+// BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
+bool prover_serial() {
+  static const bool serial = [] {
+    const char* e = getenv("BH_PROVER_SERIAL");
+    return e && e[0] == '1';
+  }();
+  return serial;
+}
+
 // When an exchanger is given (RCCL ranks, or the one-device emulation's virtual ranks) and
 // the rank count qualifies, the H block is distributed (dist_h.h): this rank's h multiexp then
 // covers the share of h it ends with instead of the range [shard*(m-1)/N, ...).
@@ -718,10 +745,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   hipStream_t sA = ctx->stream, sT = ctx->stream2, sS = ctx->stream3, sH = ctx->stream4;
   hipStream_t tails[8];
   for (int q = 0; q < 8; q++) tails[q] = ctx->tstream[q % bh_ctx::TAIL_STREAMS];
-  static const bool serial = [] {  // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
-    const char* e = getenv("BH_PROVER_SERIAL");
-    return e && e[0] == '1';
-  }();
+  const bool serial = prover_serial();
   if (serial) {
     sT = sS = sH = sA;
     for (auto& t : tails) t = sA;
@@ -833,6 +857,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // ---- H (prover.rs:210-234), device resident.  Where it is enqueued depends on h_mode
   // (below); only h's sort waits for it.
   auto enqueue_h = [&](hipEvent_t after) -> bh_status {
+    if (up && up->on_vector) {
+      // bh_prove: the uploading thread enqueues H on sH vector by vector, each behind its own
+      // upload; only h's sort (enqueued on sH right after this) needs the host to wait until
+      // that enqueue is done
+      if (!up->wait(2)) return up->status;
+      return BH_OK;
+    }
     BH_TRY_HIP(hipStreamWaitEvent(sH, after, 0));
     hipEventRecord(ctx->ev[0], sH);
     if (dh) {  // three all-to-alls (RCCL, or the emulation's device copies), stream-ordered on sH
@@ -1868,12 +1899,55 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
                               b_aux_density);
   if (st) return st;
   UploadSync up;
-  BH_TRY_HIP(hipEventCreateWithFlags(&up.ev[0], hipEventDisableTiming));
-  BH_TRY_HIP(hipEventCreateWithFlags(&up.ev[1], hipEventDisableTiming));
   struct EvGuard {
     UploadSync& u;
-    ~EvGuard() { for (auto e : u.ev) if (e) (void)hipEventDestroy(e); }
+    ~EvGuard() {
+      for (auto e : u.ev) if (e) (void)hipEventDestroy(e);
+      for (auto e : u.vec) if (e) (void)hipEventDestroy(e);
+      if (u.t0) (void)hipEventDestroy(u.t0);
+    }
   } evg{up};
+  BH_TRY_HIP(hipEventCreate(&up.t0));
+  BH_TRY_HIP(hipEventCreate(&up.ev[0]));
+  BH_TRY_HIP(hipEventCreate(&up.ev[1]));
+  for (auto& e : up.vec) BH_TRY_HIP(hipEventCreate(&e));
+  // H from the uploading thread: each of a, b, c is converted and transformed on the H stream
+  // as soon as its own upload has landed (stream order behind vec[v]), so H starts ~1/3 of the
+  // a, b, c upload after aux and runs beside the first accumulations, and no host thread that
+  // enqueues the multiexps ever waits for the upload of a, b, c (prover.rs:210-231).
+  // BH_PROVE_H_UPLOADER=0: H enqueued by compute_msms after the whole upload (round-4 scheme).
+  static const bool h_uploader = [] {
+    const char* e = getenv("BH_PROVE_H_UPLOADER");
+    return !(e && e[0] == '0') && !prover_serial();
+  }();
+  Domain* D = nullptr;
+  if (h_uploader) {
+    // everything the H stages touch, allocated before the uploading thread can enqueue them
+    if ((st = ctx_domain(ctx, w->log_m, &D))) return st;
+    BH_TRY_HIP(ctx->staging.alloc(3 * w->m * 32));
+    BH_TRY_HIP(ctx->hbuf.alloc(w->m * 32));
+    up.on_vector = [ctx, w, D, &up](int v) -> int {
+      hipStream_t sH = ctx->stream4;
+      const size_t m = w->m, nc = w->num_constraints;
+      uint32_t* abc = ctx->staging.as<uint32_t>();
+      BH_TRY_HIP(hipStreamWaitEvent(sH, up.vec[v], 0));
+      if (v == 0) BH_TRY_HIP(hipEventRecord(ctx->ev[0], sH));
+      // bls12_381 Montgomery -> device Montgomery into the H block's buffer, zero padding
+      if (nc) launch_fr_convert(w->abc.as<uint32_t>() + (size_t)v * m * 8, abc + (size_t)v * m * 8, nc,
+                                fr_to_dev_const(), 0, sH);
+      if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
+      BH_TRY_HIP(hipGetLastError());
+      bh_status hs = run_h_vector(ctx, D, abc, sH, nullptr, v);
+      if (hs) return hs;
+      if (v == 2) {
+        // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
+        if ((hs = run_h_final(ctx, D, abc, sH, ctx->hbuf.as<uint32_t>()))) return hs;
+        BH_TRY_HIP(hipEventRecord(ctx->ev[1], sH));
+      }
+      return BH_OK;
+    };
+  }
+  BH_TRY_HIP(hipEventRecord(up.t0, ctx->h2d));
   bh_status ust = BH_OK;
   std::thread uploader([&] {
     if (hipSetDevice(ctx->device) != hipSuccess) { ust = BH_ERR_HIP; up.set(-1, ust); return; }
@@ -1887,6 +1961,15 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
   (void)hipStreamSynchronize(ctx->h2d);
   if (st) return st;
   if (ust) return ust;
+  // upload landing times from the call's start (bh_last_stats [13..16): aux, a, b, c) and, from
+  // compute_msms, the H block's end ([12] stays the table bytes)
+  {
+    float t = 0;
+    ctx->last_timings[13] = hipEventElapsedTime(&t, up.t0, up.ev[0]) == hipSuccess ? t : -1;
+    for (int v = 0; v < 3; v++)
+      ctx->last_timings[14 + v] = hipEventElapsedTime(&t, up.t0, up.vec[v]) == hipSuccess ? t : -1;
+    ctx->last_timings[17] = hipEventElapsedTime(&t, up.t0, ctx->ev[1]) == hipSuccess ? t : -1;
+  }
   assemble_finish(pre.get(), r1, r2, proof_out);
   ctx->last_timings[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return BH_OK;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <functional>
 #include <mutex>
 
 #include "host_pool.h"
@@ -30,13 +31,19 @@ struct H2DRing {
 
 // Progress of an asynchronous witness upload, for the prover's streams to wait on: stage 1 =
 // density maps, inputs and aux enqueued (ev[0] recorded after them), stage 2 = a, b, c
-// enqueued (ev[1]).  A failed upload ends in stage -1 with its status.
+// enqueued (ev[1]; vec[v] right after vector v).  A failed upload ends in stage -1 with its
+// status.  on_vector, when set, runs on the uploading thread right after vector v's copies are
+// enqueued and vec[v] recorded (bh_prove: that vector's H transforms, stream-ordered behind
+// vec[v]); stage 2 is set only after the last call returned, so it then also means "H enqueued".
 struct UploadSync {
   std::mutex mu;
   std::condition_variable cv;
   int stage = 0;
   int status = 0;
+  hipEvent_t t0 = nullptr;  // recorded on the copy stream before the first copy (timing)
   hipEvent_t ev[2] = {};
+  hipEvent_t vec[3] = {};
+  std::function<int(int v)> on_vector;
   void set(int s, int st = 0) {
     std::lock_guard<std::mutex> lk(mu);
     stage = s;

@@ -427,13 +427,17 @@ def main():
         p0 = bh.prove(ctx, params, asg, r, s)
         ctx.synchronize()
         t0 = time.perf_counter()
+        landed = []
         for _ in range(args.steps):
             pd = bh.prove(ctx, params, asg, r, s)
+            landed.append([round(x, 2) for x in ctx.last_stats()[13:18]])
         ctx.synchronize()
         dms = (time.perf_counter() - t0) * 1000.0 / args.steps
         wbytes = sum(int(v.nbytes) for v in asg.values())
         dropin = {"value": round(n_constraints / (dms / 1e3), 1), "unit": "constraints/s", "ms_per_step": round(dms, 3),
                   "witness_bytes": wbytes, "proof_matches": pd == p0 == ref,
+                  "landed_ms": {"fields": ["inputs+aux", "a", "b", "c", "H done"], "per_call": landed,
+                                "source": "device events on the copy and H streams, ms from the call's start"},
                   "note": "bh_prove from host (pageable) buffers: witness upload overlapped with the proof"}
         # the proof is valid: the native verifier (verify_proof, verifier.rs:23-62) on the public
         # input (the chain's image; input 0 is ONE)

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <thread>
 
@@ -29,6 +30,16 @@ static double now_ms() {
 }
 
 __global__ void k_mark(volatile uint32_t* p) { *p = 1; }
+
+// a VALU-saturating kernel (every CU, 8 waves per SIMD) for a bounded number of iterations
+__global__ void __launch_bounds__(256) k_busy(uint64_t* out, int iters) {
+  uint64_t x = threadIdx.x + blockIdx.x, y = x * 3 + 1;
+  for (int i = 0; i < iters; i++) {
+    x = x * y + 7;
+    y = y * x + 11;
+  }
+  if (x == 0x12345) out[0] = y;
+}
 
 int main(int argc, char** argv) {
   const size_t bytes = (size_t)(argc > 1 ? atoi(argv[1]) : 128) << 20;
@@ -73,6 +84,47 @@ int main(int argc, char** argv) {
     printf("staging ring (4 x 16 MB), %2d thr %7.2f ms  %6.1f GB/s\n", pool.size(), t, rate(t));
     ring.release();
   }
+  {
+    // the same copies while every CU is saturated by a kernel on another stream (the proof's
+    // situation: the accumulations hold every SIMD)
+    hipStream_t sb;
+    CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+    uint64_t* junk;
+    CK(hipMalloc(&junk, 64));
+    hipEvent_t b0, b1;
+    CK(hipEventCreate(&b0));
+    CK(hipEventCreate(&b1));
+    CK(hipEventRecord(b0, sb));
+    k_busy<<<256 * 32, 256, 0, sb>>>(junk, 1 << 14);
+    CK(hipEventRecord(b1, sb));
+    CK(hipEventSynchronize(b1));
+    float bms = 0;
+    CK(hipEventElapsedTime(&bms, b0, b1));
+    const int iters = (int)((1 << 14) * (400.0 / std::max(bms, 0.01f)));  // ~400 ms
+    printf("busy kernel: %.1f ms at 2^14 iterations -> %d iterations\n", bms, iters);
+    bh::HostPool pool(7);
+    bh::H2DRing ring;
+    for (int rep = 0; rep < 2; rep++) {
+      k_busy<<<256 * 32, 256, 0, sb>>>(junk, iters);
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      double ta = now_ms();
+      CK(hipMemcpyAsync(dev, pin, bytes, hipMemcpyHostToDevice, st));
+      CK(hipStreamSynchronize(st));
+      double tp = now_ms() - ta;
+      ta = now_ms();
+      CK(hipMemcpy(dev, host, bytes, hipMemcpyHostToDevice));
+      double tq = now_ms() - ta;
+      ta = now_ms();
+      CK(ring.copy(pool, dev, host, bytes, st));
+      CK(hipStreamSynchronize(st));
+      double tr = now_ms() - ta;
+      const bool busy = hipStreamQuery(sb) == hipErrorNotReady;
+      printf("under a busy GPU (still busy after: %d): pinned DMA %.2f ms %.1f GB/s, pageable %.2f ms %.1f GB/s, "
+             "ring %.2f ms %.1f GB/s\n", (int)busy, tp, rate(tp), tq, rate(tq), tr, rate(tr));
+      CK(hipStreamSynchronize(sb));
+    }
+    ring.release();
+  }
   double t0 = now_ms();
   CK(hipHostRegister(host, bytes, hipHostRegisterDefault));
   double treg = now_ms() - t0;
@@ -87,13 +139,13 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, 0);
   printf("hipDeviceAttributeCanUseStreamWaitValue = %d\n", can);
   uint32_t* sig = nullptr;
-  hipError_t e = hipExtMallocWithFlags((void**)&sig, 64, hipMallocSignalMemory);
+  hipError_t e = hipExtMallocWithFlags((void**)&sig, 8, hipMallocSignalMemory);
   printf("hipExtMallocWithFlags(hipMallocSignalMemory) -> %s\n", hipGetErrorString(e));
   if (e == hipSuccess) {
     uint32_t* mark;
     CK(hipHostMalloc(&mark, 64, hipHostMallocCoherent));
     *(volatile uint32_t*)mark = 0;
-    CK(hipMemsetAsync(sig, 0, 64, st));
+    CK(hipMemsetAsync(sig, 0, 8, st));
     CK(hipStreamSynchronize(st));
     hipEvent_t done;
     CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
