@@ -614,15 +614,29 @@ static bh_status run_fft(bh_ctx* ctx, Domain* D, FftKind kind, uint32_t* d_a, ui
 static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind kind) {
   if (!ctx || !coeffs || log_m >= 32) return BH_ERR_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  BH_TRY_HIP(hipSetDevice(ctx->device));
   Domain* D;
   bh_status s = ctx_domain(ctx, (int)log_m, &D);
   if (s) return s;
   const size_t m = (size_t)1 << log_m;
   BH_TRY_HIP(ctx->staging.alloc(m * 32));
   BH_TRY_HIP(ctx->staging2.alloc(m * 32));
+  // device events around the three phases (bh_last_stats [18..21): upload, transform, download ms)
+  for (auto& e : ctx->fft_ev)
+    if (!e) BH_TRY_HIP(hipEventCreate(&e));
+  BH_TRY_HIP(hipEventRecord(ctx->fft_ev[0], ctx->stream));
   if ((s = upload_fr(ctx, coeffs, m, m, ctx->staging.as<uint32_t>()))) return s;
+  BH_TRY_HIP(hipEventRecord(ctx->fft_ev[1], ctx->stream));
   if ((s = run_fft(ctx, D, kind, ctx->staging.as<uint32_t>(), ctx->staging2.as<uint32_t>()))) return s;
-  return download_fr(ctx, ctx->staging.as<uint32_t>(), m, coeffs);
+  BH_TRY_HIP(hipEventRecord(ctx->fft_ev[2], ctx->stream));
+  if ((s = download_fr(ctx, ctx->staging.as<uint32_t>(), m, coeffs))) return s;
+  BH_TRY_HIP(hipEventRecord(ctx->fft_ev[3], ctx->stream));
+  BH_TRY_HIP(hipEventSynchronize(ctx->fft_ev[3]));
+  for (int k = 0; k < 3; k++) {
+    float t = 0;
+    ctx->last_timings[18 + k] = hipEventElapsedTime(&t, ctx->fft_ev[k], ctx->fft_ev[k + 1]) == hipSuccess ? t : -1;
+  }
+  return BH_OK;
 }
 
 // H pipeline (prover.rs:210-231) on device-resident a|b|c (3*m packed device form, natural
@@ -872,6 +886,8 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   }
   ctx_sync_all(ctx);  // nothing may still read the workspaces released below (jobs' too)
   bh_ctx_release_jobs(ctx);
+  for (auto& e : ctx->fft_ev)
+    if (e) (void)hipEventDestroy(e);
   ctx->bg.ring.release();  // (waits for its slots' copies on bg.cst)
   if (ctx->bg.st) (void)hipStreamDestroy(ctx->bg.st);
   if (ctx->bg.cst) (void)hipStreamDestroy(ctx->bg.cst);

@@ -267,6 +267,7 @@ struct bh_ctx {
   bh::DevBuf idx3;        // density index maps of a_aux | b_input | b_aux
   hipEvent_t ev[16] = {};
   double last_timings[24] = {};  // bh_last_timings [0,10) + bh_last_stats extras
+  hipEvent_t fft_ev[4] = {};     // bh_fft & co.: upload / transform / download boundaries
   uint32_t* host_counts = nullptr;  // pinned: [0,16) entries (= mixed additions) of each prover multiexp
   uint32_t* host_spans = nullptr;   // pinned: MAX_SPAN_BLOCKS per-workgroup max_span words per prover multiexp
   bh::DevBuf dspan;                 // device words for max_span (the same layout)

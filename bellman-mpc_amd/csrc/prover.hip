@@ -1176,6 +1176,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // by the host's ~0.4 ms of H enqueueing (mode 1), and H's first kernels reach the device
   // before the first accumulation fills every CU (mode 3)
   if (h_mode == 4 && (s = enqueue_h(jev[33]))) return s;
+  static const bool first_own = [] {
+    const char* e = getenv("BH_FIRST_ACC_STREAM");
+    return !(e && e[0] == '0');
+  }();
   if (nbig > 0) {
     // wait for the last pre-sort that is a real sort: a trailing copy of another multiexp's
     // entries (b_g1_aux from b_g2_aux) is ~0.15 ms of blits that can run beside the accumulation
@@ -1186,13 +1190,27 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     // stream (idle when the public-input multiexps are on the host), so the G1 accumulations start
     // beside it instead of after it: same-box A/B at 2^22 54.66-55.17 against 55.01-55.45 ms
     // (profiles/r04_ab_first_acc_stream.txt).  BH_FIRST_ACC_STREAM=0: on the main stream.
-    static const bool first_own = [] {
-      const char* e = getenv("BH_FIRST_ACC_STREAM");
-      return !(e && e[0] == '0');
-    }();
     hipStream_t s0 = (first_own && nsmall == 0 && !serial) ? sT : sA;
     BH_TRY_HIP(hipStreamWaitEvent(s0, jev[16 + wait_j], 0));
     if ((s = acc_job(big[0], s0))) return s;
+  }
+  // With the first accumulation on its own stream, the second one (G1: b_g1_aux, whose sorted
+  // entries are a copy among the first sorts) is enqueued right behind it, before the remaining
+  // sorts and H: those are ~20-40 host enqueues (~0.7 ms per rank at N = 8 in the round-5 kernel
+  // trace, 1.6 ms at N = 2), during which the G2 accumulation ran alone on its one wave per SIMD.
+  // BH_G1_EARLY=0: after the remaining sorts (round 4).
+  static const bool g1_early = [] {
+    const char* e = getenv("BH_G1_EARLY");
+    return !(e && e[0] == '0');
+  }();
+  int q_first = 1;
+  if (g1_early && nbig > 1 && !jobs[big[1]].is_h && !serial && first_own && nsmall == 0) {
+    bool pre = false;  // its sort is among the pre-sorts (enqueued above)
+    for (int r = 0; r < pre_sorts; r++) pre = pre || sorder[r] == big[1];
+    if (pre) {
+      if ((s = acc_job(big[1], sA))) return s;
+      q_first = 2;
+    }
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
   if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
@@ -1205,7 +1223,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   const auto t_sorts = std::chrono::steady_clock::now();
   bool h_done = !h_late;
-  for (int q = 1; q < nbig; q++) {
+  for (int q = q_first; q < nbig; q++) {
     if (!h_done && jobs[big[q]].is_h) {
       if ((s = enqueue_h(jev[33]))) return s;
       if ((s = sort_h_or(big[q]))) return s;

@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--c5-lanes", type=int, default=0, help="bh_prove_batch lanes per GPU (0: library default)")
     ap.add_argument("--seam", type=int, default=1,
                     help="with --dropin: also time the multiexp-level seam (bellman_hip.prove_seam)")
+    ap.add_argument("--domain", type=int, default=1,
+                    help="with --dropin: also time the EvaluationDomain seam (ifft, coset_fft, the H block) from "
+                         "host buffers")
     ap.add_argument("--dropin", type=int, default=1,
                     help="also time bh_prove from host buffers (the drop-in path; 1-GPU runs)")
     return ap.parse_args()
@@ -204,6 +207,62 @@ def c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier):
             "value": round(args.c5 * n_c / el, 1), "unit": "constraints/s", "proofs": args.c5,
             "ms_per_proof": round(el * 1e3 / max(1, len(mine)), 3), "batch_s": round(el, 3),
             "lanes": args.c5_lanes or int(os.environ.get("BH_BATCH_LANES", "2")), "proofs_match_single": ok, "synthesis_s": round(t_syn, 2)}
+
+
+def domain_leg(bh, ctx, asg, n_constraints, reps=2):
+    """The EvaluationDomain seam (domain.rs:81-189) at the bench's size from host buffers: one
+    ifft and one coset_fft (each: upload, device transform, download; the split from device
+    events), and the H block of create_proof as prover.rs:210-231 drives it through that seam
+    (3 x (ifft, coset_fft), mul_assign, sub_assign, divide_by_z_on_coset, icoset_fft: ten host
+    calls), against bh_compute_h (one call) on the same a, b, c; the two h vectors must agree."""
+    import numpy as np
+    a0, b0, c0 = (np.ascontiguousarray(asg[k]) for k in ("a", "b", "c"))
+    d = bh.EvaluationDomain(ctx, a0)
+    out = {"log_m": d.exp, "m": d.m}
+    for name in ("ifft", "coset_fft"):
+        best, split = None, None
+        for _ in range(reps + 1):
+            d.coeffs[: a0.shape[0]] = a0
+            t0 = time.perf_counter()
+            getattr(d, name)()
+            ms = (time.perf_counter() - t0) * 1e3
+            if best is None or ms < best:
+                best, split = ms, ctx.last_stats()[18:21]
+        out[name] = {"ms": round(best, 3), "upload_ms": round(split[0], 3), "transform_ms": round(split[1], 3),
+                     "download_ms": round(split[2], 3),
+                     "host_share": round((split[0] + split[2]) / best, 3) if best else None}
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        A, B, C = (bh.EvaluationDomain(ctx, x) for x in (a0, b0, c0))
+        for D_ in (A, B, C):
+            D_.ifft()
+            D_.coset_fft()
+        A.mul_assign(B)
+        A.sub_assign(C)
+        A.divide_by_z_on_coset()
+        A.icoset_fft()
+        ms = (time.perf_counter() - t0) * 1e3
+        best = ms if best is None else min(best, ms)
+    h_seam = A.coeffs[: A.m - 1].copy()
+    del A, B, C
+    import ctypes
+    h = np.zeros((d.m - 1, 4), dtype=np.uint64)
+    hl = ctypes.c_size_t()
+    hbest = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        bh._check(bh._lib.bh_compute_h(ctx.h, bh._ptr(a0), bh._ptr(b0), bh._ptr(c0), a0.shape[0], bh._ptr(h),
+                                       ctypes.byref(hl)), "bh_compute_h")
+        ms = (time.perf_counter() - t0) * 1e3
+        hbest = ms if hbest is None else min(hbest, ms)
+    out["h_via_domain_seam"] = {"ms": round(best, 3), "calls": 10,
+                                "value": round(n_constraints / (best / 1e3), 1), "unit": "constraints/s"}
+    out["h_via_bh_compute_h"] = {"ms": round(hbest, 3), "calls": 1}
+    out["h_equal"] = bool(np.array_equal(h_seam, h[: hl.value]))
+    out["note"] = ("host (Montgomery) buffers in and out of every call; each transform moves 2 x m x 32 B over "
+                   "PCIe, which is most of its time (host_share)")
+    return out
 
 
 def main():
@@ -465,6 +524,8 @@ def main():
                               "proof_matches": ps == s0 == ref,
                               "note": "prove_seam: h on the device, assignments uploaded once, 8 multiexp "
                                       "jobs on the Parameters' vectors (window tables), host assembly"}
+        if args.domain:
+            dropin["domain_seam"] = domain_leg(bh, ctx, asg, n_constraints)
         del asg
     # CPU baseline: rank 0 of a 1-GPU run only (a bounded sample; see cpu_baseline)
     base = (cpu_baseline(bh, ctx, args.cpu_log_constraints, args.cpu_1t_log_constraints,
