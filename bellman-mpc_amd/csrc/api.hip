@@ -774,9 +774,21 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   // puts them at the default priority (A/B experiments)
   const char* pe = getenv("BH_SIDE_PRIORITY");
   const int side = (pe && pe[0] == '0') ? prio_lo : prio_hi;
+  // (A/B) BH_MAIN_PRIORITY=1: the main stream (the G1 accumulations) at high priority too;
+  // BH_H_PRIORITY=0: the H stream at the default priority
+  const char* me = getenv("BH_MAIN_PRIORITY");
+  const char* he = getenv("BH_H_PRIORITY");
+  const int hprio = (he && he[0] == '0') ? prio_lo : side;
+  if (me && me[0] == '1') {
+    (void)hipStreamDestroy(c->stream);
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      release_mask(c); delete c;
+      return BH_ERR_HIP;
+    }
+  }
   if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, hprio) != hipSuccess) {
     release_mask(c); delete c;
     return BH_ERR_HIP;
   }

@@ -1,9 +1,9 @@
 """Batch-affine bucket accumulation (csrc/msm_g1_aff.hip) on the GPU, through the C ABI.
 
-At the benchmark sizes (2^20 constraints and up) the G1 window-table multiexps take the affine
-levels by default, and every full-size proof test (C3 2^22 == the port's proof, C4 2^24, C5 batch
-at 2^20) covers them.  Here the plan's knobs (read from the environment on every multiexp) force
-levels at small sizes, so that the exceptional pairs -- P + P (doubling) and P + (-P) (the point at
+The levels are opt-in (BH_AFFINE / BH_AFFINE_G1 / BH_AFFINE_G2 = 1; off by default: slower than the
+XYZZ accumulation at 2^22), so the default full-size proof tests do NOT cover
+them; these forced small-size tests are their coverage.  The plan's knobs (read from the environment
+on every multiexp) force levels at small sizes, so that the exceptional pairs -- P + P (doubling) and P + (-P) (the point at
 infinity, carried as a marked record) -- occur inside table buckets, at level 0 and deeper, and
 results are compared with the oracle and with the XYZZ-only accumulation (BH_AFFINE=0).
 Reference: multiexp.rs:191-223 (the bucket loop the levels replace)."""
