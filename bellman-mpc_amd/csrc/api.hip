@@ -932,9 +932,13 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
     if (ctx->stream4d) (void)hipStreamDestroy(ctx->stream4d);
     for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
   }
+  const int dev = ctx->device;
   release_mask(ctx);
   delete ctx->dist;
   delete ctx;
+  // the last context of the device gone: the pooled scalar buffers (up to 2 GiB) go with it
+  // (vectors still alive return theirs to the pool later, kept until the next drain or exit)
+  if (bh::live_contexts(dev) == 0) scalar_pool_drain(dev);
   return BH_OK;
 }
 
@@ -1185,6 +1189,16 @@ void scalar_pool_give(int device, void* p, size_t bytes) {
   }
   (void)hipSetDevice(device);
   (void)hipFree(p);
+}
+
+void scalar_pool_drain(int device) {
+  if (device < 0 || device >= 64) return;
+  ScalarPool& pl = g_scalar_pool[device];
+  std::lock_guard<std::mutex> lk(pl.mu);
+  (void)hipSetDevice(device);
+  for (auto& kv : pl.bufs) (void)hipFree(kv.second);
+  pl.bufs.clear();
+  pl.held = 0;
 }
 
 static bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out) {

@@ -163,6 +163,7 @@ constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use pla
 // behind them.  take: a buffer of at least `bytes` or null; give: keeps it (bounded) or frees it.
 extern "C" void* scalar_pool_take(int device, size_t bytes, size_t* got);
 extern "C" void scalar_pool_give(int device, void* p, size_t bytes);
+extern "C" void scalar_pool_drain(int device);  // frees every pooled buffer of the device
 
 struct bh_scalar_buf {
   bh::DevBuf d;
@@ -189,7 +190,9 @@ struct bh_scalar_buf {
       (void)hipEventSynchronize(ready);
       (void)hipEventDestroy(ready);
     }
-    // (every multiexp that read it has been waited for: the jobs hold this buffer until then)
+    // Invariant for the pool (no device sync here): nothing in flight still reads this buffer.
+    // The producer's H wrote it behind `ready` (synchronised above), and every multiexp that read
+    // it holds this shared buffer until its wait has host-synchronised the work (jobs.hip).
     if (d.p) scalar_pool_give(device, d.p, d.bytes);
     d.p = nullptr;
     d.bytes = 0;

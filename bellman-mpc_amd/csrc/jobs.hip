@@ -419,18 +419,16 @@ bh_status bh_multiexp_submit_scalars(bh_ctx* ctx, const bh_srs* bases, size_t ba
       jp->empty = true;
     }
   };
+  if (buf->owner != ctx) {
+    // the producer thread runs deferred enqueues on its own context's streams, and only that
+    // context's teardown waits for it: a vector still being produced by ANOTHER context is first
+    // waited for here (its producer has then enqueued H, stream-ordered behind `ready`), and the
+    // job takes the non-deferred path below
+    buf->wait_enqueued();
+  }
   {
     std::unique_lock<std::mutex> lk(buf->mu);
     if (!buf->enqueued) {
-      // the producer thread will run this enqueue on ctx: only the producing context's own
-      // teardown waits for that thread, so a vector still being produced by another context is
-      // refused (a submit after its bh_scalars_sync is fine from any context of the device)
-      if (buf->owner != ctx) {
-        lk.unlock();
-        give_slot(*jp->reg, jp->slot);
-        jp->slot = nullptr;
-        return BH_ERR_INVALID_ARGUMENT;
-      }
       std::vector<uint64_t> dens;  // the caller's density words are read before submit returns
       if (density_words) dens.assign(density_words, density_words + (n + 63) / 64);
       buf->deferred.push_back([work, dens = std::move(dens)](bh_status up) {

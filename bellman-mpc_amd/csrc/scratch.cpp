@@ -51,12 +51,18 @@ hsa_status_t visit_agent(hsa_agent_t a, void* p) {
 // out: [0] device scratch limit (bytes, shared by all queues; 0 = unknown), [1] current per-queue
 // threshold, [2] worst bytes/lane, [3] its per-queue need at the scratch-slot bound (bytes),
 // [4] queues counted, [5] the context's total need, [6] fits (1/0), [7] kernels checked, [8] the
-// worst kernel's per-queue need at its occupancy, [9] live contexts on the device (the limit is
-// shared by all of them: [5] x [9] bounds a device full of such contexts)
+// worst kernel's per-queue need at its occupancy, [9] live contexts on the device now (the limit is
+// shared by all of them: [5] x [9] bounds a device full of such contexts running at once).
+// Scope of the decision [6]: ONE context's queues.  Further contexts of the device -- a batch's
+// lanes (which borrow their primary's streams: no queue more) and the one-device rehearsal's
+// virtual ranks (which prove one after another) -- are counted in [9], refreshed on every call,
+// but not in [6]: callers that run several contexts' proofs concurrently on one device must
+// budget [5] x [9] themselves (bh_scratch_report exposes both).
 bh_status scratch_report(bh_ctx* ctx, uint64_t out[10], std::string* worst) {
   static std::mutex mu;  // (computed once per context, by whichever thread asks first)
   std::lock_guard<std::mutex> lk(mu);
   if (ctx->scratch_done) {
+    ctx->scratch_rep[9] = (uint64_t)std::max(1, live_contexts(ctx->device));
     memcpy(out, ctx->scratch_rep, sizeof(ctx->scratch_rep));
     if (worst) *worst = ctx->scratch_worst;
     return BH_OK;

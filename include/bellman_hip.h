@@ -128,8 +128,11 @@ bh_status bh_multiexp_wait(bh_job* job, uint8_t* out);
  * Montgomery words, like bh_multiexp), or produced by bh_compute_h_scalars -- and any number of
  * multiexps read it.  bh_compute_h_scalars returns at once: a host thread uploads a, b, c and
  * enqueues the H passes, and multiexps submitted on h meanwhile are enqueued by that thread
- * behind them, so a caller can submit in create_proof's own order (h first) without waiting.  Freeing the handle
- * is allowed while multiexps on it are in flight (they keep the device vector until their wait). */
+ * behind them, so a caller can submit in create_proof's own order (h first) without waiting.  That
+ * deferral is for submits on the producing context; a submit on another context of the device
+ * first waits (on the host) until the producer has enqueued H, then enqueues normally.  Freeing the
+ * handle is allowed while multiexps on it are in flight (they keep the device vector until their
+ * wait). */
 typedef struct bh_scalars bh_scalars;
 bh_status bh_scalars_upload(bh_ctx* ctx, const uint64_t* exponents, size_t n, int scalar_format, bh_scalars** out);
 bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c,
@@ -327,8 +330,10 @@ bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
  * queues; 0 unknown), [1] current per-queue threshold, [2] worst private segment (bytes/lane),
  * [3] its per-queue need at the scratch-slot bound (32 waves per CU), [4] queues counted, [5] the
  * context's total need, [6] fits (1/0), [7] kernels checked, [8] the worst kernel's per-queue need
- * at its occupancy, [9] live contexts on the device; worst_kernel (optional, cap bytes): that
- * kernel's name. */
+ * at its occupancy, [9] live contexts on the device (refreshed on every call); worst_kernel
+ * (optional, cap bytes): that kernel's name.  [6] decides for ONE context's queues: a caller that
+ * runs several contexts' proofs at once on one device must budget [5] x [9] itself (batch lanes
+ * borrow their primary's streams; the one-device rehearsal's ranks prove one after another). */
 bh_status bh_scratch_report(bh_ctx* ctx, uint64_t* out, size_t n, char* worst_kernel, size_t cap);
 
 #ifdef __cplusplus
