@@ -127,7 +127,7 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
                       size_t set, const uint64_t* density_words, const uint32_t* d_scalars, bool tables,
                       const JobStreams& st) {
   const uint32_t* pts = bases->pts.as<uint32_t>();
-  ws.aff = ctx->aff1.get();  // (the accumulation runs on ctx->stream, as the prover's)
+  ws.aff = ctx->aff1.get();  // (levels only on ctx->stream: job_g2_own_stream is off with them)
   bool tab = false;
   if (tables && set >= TABLE_MIN_USED) {
     std::lock_guard<std::mutex> lk(bases->win_mu);
@@ -242,9 +242,24 @@ size_t density_set(const uint64_t* density_words, size_t n) {
 // Common device work of both submits, on the job's slot stream (scalars already ordered before
 // it: d_scalars): the density map, the multiexp, the completion event.  On failure the slot
 // goes back and the job is left without one.
-JobStreams job_streams(bh_ctx* ctx) {
+// G2 jobs accumulate on the small-multiexp stream (stream2, idle under the seam), so a G2
+// accumulation runs beside the G1 ones as bh_prove's first accumulation does, instead of queueing
+// behind them on the main stream (create_proof submits b_g2_aux last: prover.rs:298-307).
+// BH_JOB_G2_STREAM=0: the main stream (round 4).  Off while batch-affine levels are enabled: they
+// share one set of level buffers (ctx->aff1) that only the main stream's order protects.
+bool job_g2_own_stream() {
+  static const bool v = [] {
+    const char* e = getenv("BH_JOB_G2_STREAM");
+    auto on = [](const char* n) { const char* x = getenv(n); return x && atoi(x) != 0; };
+    return !(e && e[0] == '0') && !on("BH_AFFINE") && !on("BH_AFFINE_G1") && !on("BH_AFFINE_G2");
+  }();
+  return v;
+}
+
+JobStreams job_streams(bh_ctx* ctx, bool g2) {
   static std::atomic<unsigned> rr{0};
-  return JobStreams{ctx->stream3, ctx->stream, ctx->tstream[rr.fetch_add(1) % bh_ctx::TAIL_STREAMS]};
+  return JobStreams{ctx->stream3, g2 && job_g2_own_stream() ? ctx->stream2 : ctx->stream,
+                    ctx->tstream[rr.fetch_add(1) % bh_ctx::TAIL_STREAMS]};
 }
 
 // the slot back after a failed enqueue: whatever was enqueued for it has drained first
@@ -252,6 +267,7 @@ void fail_slot(bh_ctx* ctx, bh_job* job) {
   (void)hipStreamSynchronize(ctx->h2d);
   (void)hipStreamSynchronize(ctx->stream3);
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream2);
   for (hipStream_t t : ctx->tstream) (void)hipStreamSynchronize(t);
   give_slot(*job->reg, job->slot);
   job->slot = nullptr;
@@ -260,7 +276,7 @@ void fail_slot(bh_ctx* ctx, bh_job* job) {
 bh_status enqueue_job(bh_ctx* ctx, bh_job* job, const bh_srs* bases, size_t base_offset,
                       const uint64_t* density_words, size_t n, const uint32_t* d_scalars, uint64_t scalars_id) {
   bh_job_slot* sl = job->slot;
-  JobStreams js = job_streams(ctx);
+  JobStreams js = job_streams(ctx, bases->group != BH_G1);
   js.key = scalars_id;
   if (scalars_id && density_words) js.dens_hash = words_hash(density_words, (n + 63) / 64) | 1u;
   auto fail = [&](bh_status e) {
