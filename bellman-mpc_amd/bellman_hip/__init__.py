@@ -138,6 +138,7 @@ def _load():
         "bh_scalars_free": (I, [P]),
         "bh_multiexp_submit_scalars": (I, [P, P, S, P, S, P, P]),
         "bh_scalars_sync": (I, [P]),
+        "bh_scalars_stamps": (I, [P, P]),
         "bh_scratch_report": (I, [P, P, S, ctypes.c_char_p, S]),
     }
     for name, (res, args) in sig.items():
@@ -164,7 +165,7 @@ EXPORTED_SYMBOLS = [
     "bh_prove_witness_partials_ranks", "bh_chain_sizes", "bh_chain_assignment", "bh_rehearse_rank",
     "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch", "bh_verify_proof", "bh_verify_batch",
     "bh_params_vector", "bh_scalars_upload", "bh_compute_h_scalars", "bh_scalars_len", "bh_scalars_free",
-    "bh_multiexp_submit_scalars", "bh_scalars_sync", "bh_scratch_report",
+    "bh_multiexp_submit_scalars", "bh_scalars_sync", "bh_scratch_report", "bh_scalars_stamps",
 ]
 BH_VEC_H, BH_VEC_L, BH_VEC_A, BH_VEC_B_G1, BH_VEC_B_G2 = range(5)
 PARTIAL_BYTES = 960
@@ -414,6 +415,13 @@ class Scalars:
         """bh_scalars_sync: the producer has read its host buffers (and reports the H status)."""
         _check(_lib.bh_scalars_sync(self.h), "bh_scalars_sync")
         self._keep = None
+
+    def stamps(self):
+        """bh_scalars_stamps: the producer's stage times (ms since compute_h_scalars): a, b, c copies
+        enqueued, H enqueued, deferred multiexps enqueued, and how many were deferred."""
+        out = (ctypes.c_double * 6)()
+        _check(_lib.bh_scalars_stamps(self.h, out), "bh_scalars_stamps")
+        return [round(x, 3) for x in out]
 
     def close(self):
         if getattr(self, "h", None):
@@ -796,7 +804,7 @@ def prove(ctx, params, asg, r, s):
     return out.tobytes()
 
 
-def prove_seam(ctx, params, asg, r, s):
+def prove_seam(ctx, params, asg, r, s, profile=None):
     """create_proof after synthesis (prover.rs:206-349) through the multiexp seam alone, as a
     Rust caller that swaps only multiexp() and the H block sees it: h on the device
     (bh_compute_h_scalars), the assignments uploaded once (the Arcs of prover.rs:233-250), the
@@ -817,6 +825,8 @@ def prove_seam(ctx, params, asg, r, s):
                multiexp_async(ctx, B1, 0, b_in, inp), multiexp_async(ctx, B1, b_in_total, b_aux, aux),
                multiexp_async(ctx, B2, 0, b_in, inp), multiexp_async(ctx, B2, b_in_total, b_aux, aux)]
     partial = b"".join(w.wait() for w in waiters)
+    if profile is not None:  # the h producer's stage times of this call (bh_scalars_stamps)
+        profile.append(h.stamps())
     return proof_from_partials(params.vk_bytes(), partial, 1, r, s)
 
 

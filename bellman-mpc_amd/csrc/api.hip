@@ -1274,7 +1274,11 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
   // The producer holds no reference to the vector (its destructor joins the producer); the
   // caller's a, b, c stay borrowed until the upload has read them (bh_scalars_sync)
   bh_scalar_buf* raw = buf.get();
-  raw->producer = std::thread([ctx, raw, a, b, c, nc, m, D] {
+  const auto t_call = std::chrono::steady_clock::now();
+  raw->producer = std::thread([ctx, raw, a, b, c, nc, m, D, t_call] {
+    auto since = [t_call] {
+      return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+    };
     auto run = [&]() -> bh_status {
       auto& bg = ctx->bg;
       std::lock_guard<std::mutex> lk(bg.mu);
@@ -1320,6 +1324,7 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
           }
           stamp("uploaded", v);
         }
+        raw->stamps[v] = since();
         BH_TRY_HIP(hipEventRecord(bg.vec[v], bg.cst));
         BH_TRY_HIP(hipStreamWaitEvent(bg.st, bg.vec[v], 0));
         if (nc) launch_fr_convert(dst, dst, nc, fr_to_dev_const(), 0, bg.st);
@@ -1330,6 +1335,7 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
       // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
       bh_status hs = run_h_final(ctx, D, abc, bg.st, raw->d.as<uint32_t>());
       if (hs) return hs;
+      raw->stamps[3] = since();
       BH_TRY_HIP(hipEventRecord(raw->ready, bg.st));
       return BH_OK;
     };
@@ -1341,7 +1347,9 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
       std::lock_guard<std::mutex> lk(raw->mu);
       raw->status = st;
       for (auto& f : raw->deferred) f(st);
+      raw->stamps[5] = (double)raw->deferred.size();
       raw->deferred.clear();
+      raw->stamps[4] = since();
       raw->enqueued = true;
     }
     raw->cv.notify_all();
@@ -1352,6 +1360,13 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
     ctx->bg.cv.notify_all();
   });
   *h_out = new bh_scalars{m - 1, std::move(buf)};
+  return BH_OK;
+}
+
+bh_status bh_scalars_stamps(bh_scalars* s, double out[6]) {
+  if (!s || !s->buf || !out) return BH_ERR_INVALID_ARGUMENT;
+  s->buf->wait_enqueued();
+  memcpy(out, s->buf->stamps, sizeof(s->buf->stamps));
   return BH_OK;
 }
 

@@ -177,6 +177,9 @@ struct bh_scalar_buf {
   std::condition_variable cv;
   bool enqueued = true;
   bh_status status = BH_OK;
+  // bh_compute_h_scalars' producer, ms since the call: [0..3) a, b, c copies enqueued, [3] H enqueued,
+  // [4] deferred multiexps enqueued, [5] submits deferred behind it
+  double stamps[6] = {-1, -1, -1, -1, -1, 0};
   std::vector<std::function<void(bh_status)>> deferred;
   std::thread producer;
   void wait_enqueued() {

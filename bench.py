@@ -515,13 +515,20 @@ def main():
             bh.prove_seam(ctx, params, asg, r, s)
             ctx.synchronize()
             t0 = time.perf_counter()
+            stamps, call_ms = [], []
             for _ in range(args.steps):
-                ps = bh.prove_seam(ctx, params, asg, r, s)
+                tc = time.perf_counter()
+                ps = bh.prove_seam(ctx, params, asg, r, s, profile=stamps)
+                call_ms.append(round((time.perf_counter() - tc) * 1e3, 2))
             ctx.synchronize()
             sms = (time.perf_counter() - t0) * 1000.0 / args.steps
             dropin["seam"] = {"value": round(n_constraints / (sms / 1e3), 1), "unit": "constraints/s",
                               "ms_per_step": round(sms, 3), "vs_dropin": round(dms / sms, 4),
                               "proof_matches": ps == s0 == ref,
+                              "per_call": {"ms": call_ms, "h_producer_ms": stamps,
+                                           "fields": "bh_scalars_stamps: a, b, c copies enqueued, H enqueued, "
+                                                     "deferred multiexps enqueued (ms since the call), "
+                                                     "multiexps deferred"},
                               "note": "prove_seam: h on the device, assignments uploaded once, 8 multiexp "
                                       "jobs on the Parameters' vectors (window tables), host assembly"}
         if args.domain:

@@ -143,6 +143,10 @@ bh_status bh_scalars_free(bh_scalars* s);
  * returns (or a multiexp on the vector has been waited, or the vector is freed).  Returns the
  * H block's status (also reported by every multiexp waited on it). */
 bh_status bh_scalars_sync(bh_scalars* s);
+/* Profile of bh_compute_h_scalars' producer (waits like bh_scalars_sync), ms since the call:
+ * [0..3) the copies of a, b, c enqueued, [3] the H passes enqueued, [4] the multiexps deferred
+ * behind it enqueued, [5] how many were deferred.  A vector from bh_scalars_upload reports -1s. */
+bh_status bh_scalars_stamps(bh_scalars* s, double out[6]);
 bh_status bh_multiexp_submit_scalars(bh_ctx* ctx, const bh_srs* bases, size_t base_offset,
                                      const uint64_t* density_words, size_t density_len, const bh_scalars* exps,
                                      bh_job** out);

@@ -923,6 +923,27 @@ def test_h_scalars_deferred_submit_and_context_teardown(ctx):
     h2.close()
 
 
+def test_h_scalars_submit_from_another_context_and_stamps(ctx):
+    """A multiexp on an h vector that ANOTHER context of the device is still producing is
+    enqueued after that producer has enqueued H (the submit waits on the host; round 4 refused
+    it), and equals the multiexp of the host-computed h; the producer's stage stamps
+    (bh_scalars_stamps) are ordered: a, b, c copies, H enqueued."""
+    bh = _bh()
+    rounds = (1 << 15) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    H = params.vector(bh.BH_VEC_H)
+    c2 = bh.Context(0)
+    h = bh.compute_h_scalars(c2, asg["a"], asg["b"], asg["c"])
+    got = bh.multiexp_async(ctx, H, 0, None, h).wait()
+    hv = bh.compute_h(ctx, asg["a"], asg["b"], asg["c"])
+    assert bh.multiexp(ctx, H, 0, None, hv) == got
+    st = h.stamps()
+    assert len(st) == 6 and 0 <= st[0] <= st[1] <= st[2] <= st[3] <= st[4]
+    h.close()
+    c2.close()
+
+
 def test_shared_sorts_follow_the_vector_not_its_address(ctx):
     """Jobs over the same bh_scalars vector share digit sorts: l's full-density sort is compacted
     through b_aux's density map for b_g1_aux (the prover's derived sort), and b_g2_aux (same vector,
