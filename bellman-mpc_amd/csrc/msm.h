@@ -179,6 +179,7 @@ template <class C>
 void msm_acc_kernels(std::vector<KernInfo>& v);
 template <class C>
 void msm_back_kernels(std::vector<KernInfo>& v);
+size_t reduce_blocks_resident_per_cu_g1();  // (msm_g1_back.hip)
 void aff_kernels_g1(std::vector<KernInfo>& v);
 void aff_kernels_g2(std::vector<KernInfo>& v);
 // max over buckets of (last segment - first segment) for segment length S: the

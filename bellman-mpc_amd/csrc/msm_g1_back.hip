@@ -21,4 +21,16 @@ template hipError_t msm_front<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, const ui
                                    const int32_t*, uint32_t, const MsmShape&, MsmTiming*);
 template hipError_t msm_back<G1Ops>(MsmWorkspace<G1Ops>&, hipStream_t, size_t, const MsmShape&, typename G1Ops::P*, int, hipEvent_t, const uint32_t*);
 template void msm_back_kernels<G1Ops>(std::vector<KernInfo>&);
+
+// resident threads per CU of the G1 bucket reduction at its launch shape (msm_back: 256-thread
+// blocks, one point of LDS per thread)
+size_t reduce_blocks_resident_per_cu_g1() {
+  int blocks = 1;
+  const int BT = (int)reduce_block_max(false);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, (const void*)k_reduce_blocks<G1Ops>, BT,
+                                                   BT * sizeof(typename G1Ops::P)) != hipSuccess ||
+      blocks < 1)
+    blocks = 1;
+  return (size_t)blocks * BT;
+}
 }  // namespace bh

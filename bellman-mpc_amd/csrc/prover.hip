@@ -666,6 +666,19 @@ bool prover_serial() {
   return serial;
 }
 
+// resident threads of the G1 bucket reduction (k_reduce_blocks) on every CU (full) or on the
+// CU-masked tail streams' quarter of them
+size_t reduce_resident_threads(bh_ctx* ctx, bool full) {
+  static size_t per_cu = 0;
+  static int ncu = 0;
+  if (!per_cu) {
+    per_cu = reduce_blocks_resident_per_cu_g1();
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  }
+  const int cus = full ? ncu : std::max(1, ncu / 4);
+  return per_cu * (size_t)std::max(cus, 1);
+}
+
 // When an exchanger is given (RCCL ranks, or the one-device emulation's virtual ranks) and
 // the rank count qualifies, the H block is distributed (dist_h.h): this rank's h multiexp then
 // covers the share of h it ends with instead of the range [shard*(m-1)/N, ...).
@@ -750,6 +763,17 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     sT = sS = sH = sA;
     for (auto& t : tails) t = sA;
   }
+  // The last multiexp's reduction tail runs when every accumulation is done, alone at the end of
+  // the critical path: on the CU-masked tail streams (a quarter of the CUs) its 2^19-bucket
+  // reduction needed two rounds of resident blocks.  BH_LAST_TAIL_FULL (default on, not on a
+  // pipelined batch lane, whose next proof's first accumulation would queue behind it): on the
+  // small-multiexp stream (high priority, every CU), with its bucket reduction shaped for one round
+  // of the whole GPU.
+  static const bool last_full_env = [] {
+    const char* e = getenv("BH_LAST_TAIL_FULL");
+    return !(e && e[0] == '0');
+  }();
+  const bool last_full = last_full_env && !serial && !ctx->borrowed_streams && ctx->cu_masked;
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated,
                                // [32] start, [33] density maps ready
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
@@ -1066,10 +1090,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // the earlier tails, which share the SIMDs with accumulations, keep the work-lean shape.
   if (nbig > 0) {
     MsmShape& sl = shapes[big[nbig - 1]];
-    static const int last_threads = [] {
+    static const int last_threads_env = [] {
       const char* e = getenv("BH_LAST_TAIL_THREADS");
-      return e ? atoi(e) : 65536;
+      return e ? atoi(e) : 0;
     }();
+    // default: one round of resident k_reduce_blocks blocks on the CUs the last tail runs on
+    const int last_threads = last_threads_env ? last_threads_env
+                             : last_full       ? (int)std::min<size_t>(reduce_resident_threads(ctx, true), 1 << 20)
+                                               : 65536;
     // BH_LAST_HALVES=1: with one shared bucket window, the last multiexp is accumulated as two
     // bucket halves and the lower half's reduction (work-lean L) runs beside the upper half's
     // accumulation: only the upper half's, with the short chains, is left at the end.  Parity
@@ -1250,6 +1278,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   const auto t_hand = std::chrono::steady_clock::now();
   if (t_lane.after_accs) t_lane.after_accs();
   if (t_lane.before_tails) t_lane.before_tails();
+  if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = sT;
   for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
     BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
