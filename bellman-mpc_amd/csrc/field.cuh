@@ -409,6 +409,86 @@ BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, cons
   r0.v[N - 1] = (uint32_t)acc0 + (C::P[N - 1] & neg) + c;
 }
 
+// a*b - c*d in Fp2 with ONE Montgomery reduction per half (lazy reduction over both Karatsuba
+// products): per column t0 = sum a0 b0, t1 = sum a1 b1, t2 = sum (a0+a1)(b0+b1) and the same
+// u0, u1, u2 for c, d; half 0 gets (t0 - t1) - (u0 - u1), half 1 (t2 - t0 - t1) - (u2 - u0 - u1).
+// 6 x 196 product mads + 2 x 196 reduction mads instead of 2 x (3 + 2) x 196 for two products and
+// a subtraction.  Bounds (column k, in units of 2^58): operand limbs < 2^29 (normalised; values
+// < 2^386, so the top limb is < 2^9), so one product's column sum is < 13 and a half's column
+// difference lies in (-26, 26); the m*p terms add [0, 7.02) (p's own limbs: max over k of
+// (2^29-1) * sum of the p limbs the column meets, computed in DESIGN.md section 4).  The width
+// 59.02 < 64 fits 64 bits, but not signed: each accumulator carries BIAS = 28 * 2^58 (a multiple
+// of 2^29) and is read as unsigned, in (2, 61.02) * 2^58; the carry out of a column is
+// (acc >> 29) - (BIAS >> 29), i.e. the next column starts from (acc >> 29) + (BIAS - (BIAS >> 29)).
+// The result (X + M p) / R lies in (-p, 2p) for |X| < 2^25 p^2 (R = 2^406 > 2^25 p): a negative
+// half gets + p, leaving [0, 2p).
+template <class C>
+BH_DEV void fe2_mul_sub_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, const Fe<C>& b1, const Fe<C>& c0,
+                             const Fe<C>& c1, const Fe<C>& d0, const Fe<C>& d1, Fe<C>& r0, Fe<C>& r1) {
+  constexpr int N = C::N;
+  constexpr uint64_t BIAS = 7ull << 60;  // 28 * 2^58
+  constexpr uint64_t NEXT = BIAS - (BIAS >> C::BITS);
+  uint32_t m0[N], m1[N], sa[N], sb[N], sc[N], sd[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    sa[i] = a0.v[i] + a1.v[i];
+    sb[i] = b0.v[i] + b1.v[i];
+    sc[i] = c0.v[i] + c1.v[i];
+    sd[i] = d0.v[i] + d1.v[i];
+  }
+  uint64_t acc0 = BIAS, acc1 = BIAS;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    uint64_t t0 = 0, t1 = 0, t2 = 0, u0 = 0, u1 = 0, u2 = 0;
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+      t0 += (uint64_t)a0.v[i] * b0.v[k - i];
+      t1 += (uint64_t)a1.v[i] * b1.v[k - i];
+      t2 += (uint64_t)sa[i] * sb[k - i];
+      u0 += (uint64_t)c0.v[i] * d0.v[k - i];
+      u1 += (uint64_t)c1.v[i] * d1.v[k - i];
+      u2 += (uint64_t)sc[i] * sd[k - i];
+    }
+    // (two's complement: the differences are exact mod 2^64 and the biased sums are in range)
+    acc0 += (t0 - t1) - (u0 - u1);
+    acc1 += (t2 - t0 - t1) - (u2 - u0 - u1);
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) {
+      acc0 += (uint64_t)m0[i] * C::P[k - i];
+      acc1 += (uint64_t)m1[i] * C::P[k - i];
+    }
+    if (k < N) {
+      m0[k] = ((uint32_t)acc0 * C::INV) & C::MASK;
+      acc0 += (uint64_t)m0[k] * C::P[0];
+      m1[k] = ((uint32_t)acc1 * C::INV) & C::MASK;
+      acc1 += (uint64_t)m1[k] * C::P[0];
+    } else {
+      r0.v[k - N] = (uint32_t)acc0 & C::MASK;
+      r1.v[k - N] = (uint32_t)acc1 & C::MASK;
+    }
+    acc0 = (acc0 >> C::BITS) + NEXT;
+    acc1 = (acc1 >> C::BITS) + NEXT;
+#ifdef BH_FP2_COLUMN_SB
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+  // top limbs: the signed remainders (acc - BIAS); a negative half gets + p
+  const int64_t top0 = (int64_t)(acc0 - BIAS), top1 = (int64_t)(acc1 - BIAS);
+  const uint32_t neg0 = (uint32_t)(top0 >> 63), neg1 = (uint32_t)(top1 >> 63);
+  uint32_t cy0 = 0, cy1 = 0;
+#pragma unroll
+  for (int i = 0; i < N - 1; i++) {
+    const uint32_t s0 = r0.v[i] + (C::P[i] & neg0) + cy0;
+    r0.v[i] = s0 & C::MASK;
+    cy0 = s0 >> C::BITS;
+    const uint32_t s1 = r1.v[i] + (C::P[i] & neg1) + cy1;
+    r1.v[i] = s1 & C::MASK;
+    cy1 = s1 >> C::BITS;
+  }
+  r0.v[N - 1] = (uint32_t)top0 + (C::P[N - 1] & neg0) + cy0;
+  r1.v[N - 1] = (uint32_t)top1 + (C::P[N - 1] & neg1) + cy1;
+}
+
 constexpr uint32_t bh_pow2_ceil_fp2(uint32_t x) {
   uint32_t r = 1;
   while (r < x) r <<= 1;
@@ -452,6 +532,13 @@ struct Fp2Ops {
   // a*b - c*d (c unused as a bound here: both products are reduced, < MB*p each)
   template <uint32_t K> static BH_DEV T mul_sub(const T& a, const T& b, const T& c, const T& d) {
     return sub<bh_pow2_ceil_fp2(MB)>(mul(a, b), mul(c, d));
+  }
+  // the same with one reduction per half over both Karatsuba products (fe2_mul_sub_kara): < 2p,
+  // for operands whose values are < 2^386 with normalised limbs
+  static BH_DEV T mul_sub_lazy(const T& a, const T& b, const T& c, const T& d) {
+    T r;
+    fe2_mul_sub_kara<FpCfg>(a.c0, a.c1, b.c0, b.c1, c.c0, c.c1, d.c0, d.c1, r.c0, r.c1);
+    return r;
   }
   static BH_DEV bool is_zero(const T& a) { return fe_is_zero<FpCfg>(a.c0) && fe_is_zero<FpCfg>(a.c1); }
   static BH_DEV T zero() { return T{fe_zero<FpCfg>(), fe_zero<FpCfg>()}; }

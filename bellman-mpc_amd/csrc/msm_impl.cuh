@@ -618,10 +618,16 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
     const T Q2 = F::add(Q, Q);
     const T X3 = F::template sub<Cv::K1>(F::sqr(R), twice ? Q2 : F::add(PPP, Q2));
     G2_SB();
-    if constexpr (std::is_same<F, Fp2Ops>::value) {  // (two products: one at a time)
+    if constexpr (std::is_same<F, Fp2Ops>::value) {
+#ifndef BH_G2_Y3_TWO_PRODUCTS
+      // one reduction per half for both Karatsuba products (fe2_mul_sub_kara): R < 6p,
+      // Q - X3 + 16p < 18p, Y < 4p, PPP < 2p, all < 2^386 with normalised limbs; Y3 < 2p
+      Y = F::mul_sub_lazy(R, F::template sub<Cv::K2>(Q, X3), Y, PPP);
+#else  // (A/B) two products, one at a time, then a subtraction: < 4p
       const T RQ3 = F::mul(R, F::template sub<Cv::K2>(Q, X3));
       G2_SB();
-      Y = F::template sub<2>(RQ3, F::mul(Y, PPP));  // < 4p
+      Y = F::template sub<2>(RQ3, F::mul(Y, PPP));
+#endif
     } else {  // one reduction for both products (fe_mul2)
       Y = F::template mul_sub<Cv::KY>(R, F::template sub<Cv::K2>(Q, X3), Y, PPP);
     }
