@@ -758,7 +758,6 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   BH_TRY_HIP(hipSetDevice(device));
   bh_ctx* c = new bh_ctx();
   c->device = device;
-  c->attach_affine();
   if (device < 64) {
     g_live_ctxs[device]++;
     c->counted = true;
@@ -868,8 +867,6 @@ __attribute__((visibility("hidden"))) bh_status ctx_create_lane(bh_ctx* primary,
   for (int q = 0; q < bh_ctx::TAIL_STREAMS; q++) c->tstream[q] = primary->tstream[q];
   c->tables = primary->tables;
   c->window_override = primary->window_override;
-  c->aff1 = primary->aff1;
-  c->attach_affine();
   bool ok = true;
   for (auto& e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   for (auto& e : c->jev) ok = ok && hipEventCreate(&e) == hipSuccess;

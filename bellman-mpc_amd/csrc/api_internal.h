@@ -250,15 +250,6 @@ struct bh_ctx {
   // tails of different multiexps never share buffers (about 1 GB each at 2^22 points)
   bh::MsmWorkspace<G1Ops> pw1[6];
   bh::MsmWorkspace<G2Ops> pw2[2];
-  // batch-affine level buffers of the G1 and G2 accumulations on `stream` (msm.h; shared with the
-  // lanes that borrow this context's streams: the main stream serialises their use)
-  std::shared_ptr<bh::AffineBufs> aff1 = std::make_shared<bh::AffineBufs>();
-  void attach_affine() {
-    for (auto& w : pw1) w.aff = aff1.get();
-    for (auto& w : pw2) w.aff = aff1.get();
-    g1ws.aff = aff1.get();
-    g2ws.aff = aff1.get();
-  }
   XYZZ<G1F>* host_out1 = nullptr;     // pinned, 8 jobs x 128 windows (c >= 2)
   XYZZ<Fp2Ops>* host_out2 = nullptr;  // pinned, 2 jobs x 128 windows
   hipEvent_t jev[48] = {};

@@ -127,7 +127,6 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
                       size_t set, const uint64_t* density_words, const uint32_t* d_scalars, bool tables,
                       const JobStreams& st) {
   const uint32_t* pts = bases->pts.as<uint32_t>();
-  ws.aff = ctx->aff1.get();  // (levels only on ctx->stream: job_g2_own_stream is off with them)
   bool tab = false;
   if (tables && set >= TABLE_MIN_USED) {
     std::lock_guard<std::mutex> lk(bases->win_mu);
@@ -245,13 +244,11 @@ size_t density_set(const uint64_t* density_words, size_t n) {
 // G2 jobs accumulate on the small-multiexp stream (stream2, idle under the seam), so a G2
 // accumulation runs beside the G1 ones as bh_prove's first accumulation does, instead of queueing
 // behind them on the main stream (create_proof submits b_g2_aux last: prover.rs:298-307).
-// BH_JOB_G2_STREAM=0: the main stream (round 4).  Off while batch-affine levels are enabled: they
-// share one set of level buffers (ctx->aff1) that only the main stream's order protects.
+// BH_JOB_G2_STREAM=0: the main stream (round 4).
 bool job_g2_own_stream() {
   static const bool v = [] {
     const char* e = getenv("BH_JOB_G2_STREAM");
-    auto on = [](const char* n) { const char* x = getenv(n); return x && atoi(x) != 0; };
-    return !(e && e[0] == '0') && !on("BH_AFFINE") && !on("BH_AFFINE_G1") && !on("BH_AFFINE_G2");
+    return !(e && e[0] == '0');
   }();
   return v;
 }

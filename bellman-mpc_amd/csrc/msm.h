@@ -72,57 +72,11 @@ struct MsmTiming {
   hipEvent_t ev_half = nullptr;  // halves: recorded once the lower half is accumulated
 };
 
-// ---- Batch-affine bucket accumulation (msm_g1_aff.hip).  Before the XYZZ accumulation, the
-// sorted entries of every bucket are added pairwise in affine coordinates, level by level
-// (entries 2j and 2j+1 of a bucket -> record j of the next level; an odd last entry is carried),
-// each thread taking K pairs of a level and sharing ONE field inversion over them (Montgomery's
-// trick; the inversion is safegcd.h's divsteps).  An affine addition costs 5M + 1S plus the
-// inversion's share, against 8M + 2S (+ the Y3 product pair) for the XYZZ mixed addition.  The
-// XYZZ accumulation then sums the last level's records (ceil(count / 2^levels) per bucket).
-// Record of a level: x then y as 14 + 14 raw 29-bit limbs (112 B); the point at infinity (a
-// P + (-P) pair) has AFF_IDENT set in x's top limb word.
-constexpr uint32_t G1_AFF_REC = 28;
-constexpr uint32_t G2_AFF_REC = 56;   // (x.c0, x.c1, y.c0, y.c1: 4 x 14 raw limbs, 224 B)
-constexpr uint32_t G2_TABLE_REC = 64; // G2 window-table record: raw-limb x, y (56 words, as G2_AFF_REC) in a 256-B line
-constexpr uint32_t AFF_IDENT = 0x80000000u;
-constexpr int AFF_LMAX = 8;
-
-// per-context level buffers (two record buffers, ping-pong, and the prefix-product scratch),
-// shared by every workspace whose accumulations run on the context's main stream (stream order
-// serialises their use); mu is held from sizing (reserve) to the last launch that reads them, so
-// a growth (hipFree synchronises the device) never frees a buffer a launch is about to take
-struct AffineBufs {
-  std::mutex mu;
-  void* pts[2] = {nullptr, nullptr};
-  size_t cap_pts[2] = {0, 0};
-  void* pre = nullptr;
-  size_t cap_pre = 0;
-  hipError_t reserve(size_t pts0, size_t pts1, size_t pre_bytes);
-  void release();
-  ~AffineBufs() { release(); }
-};
-
-// Levels of one accumulation: deterministic in (n, shape) so that the reduction (msm_back) finds
-// the same final-level geometry as the accumulation that produced it.
-struct AffinePlan {
-  int levels = 0;                 // 0: the XYZZ accumulation over the sorted entries
-  uint32_t K[AFF_LMAX] = {};      // output records per thread at each level
-  uint32_t blocks[AFF_LMAX] = {}; // workgroups of 256 at each level
-  size_t Eb[AFF_LMAX + 1] = {};   // upper bound of the records after each level (Eb[0]: entries)
-  int S = 0;                      // segment length of the XYZZ accumulation over the last level
-};
-// (nbt buckets, Emax = n*W entries at most); levels = 0 unless the context has AffineBufs, the
-// bases are a window table and the level's pairs fill at least BH_AFF_KMIN (16) per thread
-AffinePlan affine_plan_g1(size_t Emax, size_t nbt, int halves);
-AffinePlan affine_plan_g2(size_t Emax, size_t nbt, int halves);
+// G2 window-table record: raw-limb x, y (4 x 14 limbs, 56 words) in a 256-B line
+constexpr uint32_t G2_TABLE_REC = 64;
 
 template <class C>
 struct MsmWorkspace {
-  AffineBufs* aff = nullptr;  // the context's level buffers (null: no batch-affine levels)
-  // batch-affine geometry of this workspace's multiexp: per-level offsets (AFF_LMAX x (nbt+1)),
-  // the last level's counts (nbt+1), scan scratch, and the last level's max-span words
-  uint32_t *aoff = nullptr, *acnt = nullptr, *ascan = nullptr, *aspan = nullptr;
-  size_t cap_anbt = 0;
   size_t cap_n = 0, cap_E = 0, cap_nbt = 0, cap_segs = 0, cap_T = 0;
   uint32_t *entries = nullptr, *counts = nullptr, *offsets = nullptr, *cursor = nullptr, *scan_scratch = nullptr,
            *cont_bucket = nullptr, *tilecounts = nullptr, *tscan = nullptr;
@@ -180,8 +134,6 @@ void msm_acc_kernels(std::vector<KernInfo>& v);
 template <class C>
 void msm_back_kernels(std::vector<KernInfo>& v);
 size_t reduce_blocks_resident_per_cu_g1();  // (msm_g1_back.hip)
-void aff_kernels_g1(std::vector<KernInfo>& v);
-void aff_kernels_g2(std::vector<KernInfo>& v);
 // max over buckets of (last segment - first segment) for segment length S: the
 // continuation-tree depth msm_back needs.  Each of max_span_blocks(nbt) workgroups writes its
 // own maximum to d_words[b] and the (pinned) h_words receive them, stream-ordered; the host takes
@@ -214,30 +166,6 @@ size_t sort_tilecount_words(const MsmShape& sh, size_t n);
 // an already sorted source (src_off: the source's base offset; idx: the target's shard-relative
 // base-index map, -1 = absent).  pos: Emax+1 words scratch; scan_scratch: derive_scratch_words.
 size_t derive_scratch_words(size_t Emax);
-// Batch-affine levels of a G1 accumulation (msm_g1_aff.hip), stream-ordered on st after the sort:
-// fills ws.aoff/acnt/aspan and the level records; returns the final level's records (rec
-// G1_AFF_REC words each) for the XYZZ accumulation, or null when plan.levels == 0
-hipError_t affine_levels_g1(MsmWorkspace<G1Ops>& ws, hipStream_t st, const uint32_t* d_bases, uint32_t rec,
-                            const AffinePlan& plan, size_t nbt, const uint32_t** final_pts);
-hipError_t affine_levels_g2(MsmWorkspace<G2Ops>& ws, hipStream_t st, const uint32_t* d_bases, uint32_t rec,
-                            const AffinePlan& plan, size_t nbt, const uint32_t** final_pts);
-// per-workspace level geometry arrays (aoff, acnt, ascan, aspan) for nbt buckets
-template <class C>
-hipError_t affine_reserve(MsmWorkspace<C>& ws, size_t nbt) {
-  if (nbt <= ws.cap_anbt && ws.aoff) return hipSuccess;
-  for (uint32_t** p : {&ws.aoff, &ws.acnt, &ws.ascan, &ws.aspan}) {
-    if (*p) (void)hipFree(*p);
-    *p = nullptr;
-  }
-  ws.cap_anbt = 0;
-  hipError_t e;
-  if ((e = hipMalloc(&ws.aoff, (size_t)AFF_LMAX * (nbt + 1) * 4)) != hipSuccess) return e;
-  if ((e = hipMalloc(&ws.acnt, (nbt + 1) * 4)) != hipSuccess) return e;
-  if ((e = hipMalloc(&ws.ascan, scan_scratch_words(nbt + 1) * 4 + 64)) != hipSuccess) return e;
-  if ((e = hipMalloc(&ws.aspan, MAX_SPAN_BLOCKS * 4)) != hipSuccess) return e;
-  ws.cap_anbt = nbt;
-  return hipSuccess;
-}
 hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offsets, size_t nbt, size_t Emax, int pre,
                          uint32_t W, uint32_t src_off, const int32_t* idx, uint32_t* pos, uint32_t* scan_scratch,
                          uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st);

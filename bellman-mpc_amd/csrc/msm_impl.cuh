@@ -571,11 +571,6 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
     }
     if constexpr (!DIRECT) __builtin_amdgcn_s_waitcnt(0x3f70);  // vmcnt(0): base j has landed in LDS
     const T x2 = base_coord(0);
-    // (a batch-affine level record of the point at infinity: word 13 of x, limbs only)
-    if (limbs && (reinterpret_cast<const uint32_t*>(&x2)[13] & AFF_IDENT)) {
-      (void)take_y(j);
-      continue;
-    }
     if (ident) {
       Y = take_y(j);
       X = x2;
@@ -657,11 +652,9 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   constexpr bool G1 = std::is_same<C, G1Ops>::value;
   constexpr int NW = sizeof(typename F::T) / 4;    // raw limb words per coordinate (G1: 14)
   constexpr int NQ = NW / 2;                       // 16-byte pieces per raw-limb base (G1 7, G2 14)
-  // Window-table records hold raw limbs (G1_TABLE_REC 7 pieces, G2_TABLE_REC 14: no unpacking), and so do the
-  // batch-affine levels' records (G1_AFF_REC / G2_AFF_REC: read in order, entries == null; a
-  // record of the point at infinity, AFF_IDENT in word 13, is skipped); plain vectors are packed
-  // (6 / 12 pieces)
-  const bool limbs = G1 ? (rec == G1_TABLE_REC || rec == G1_AFF_REC) : (rec == G2_TABLE_REC || rec == G2_AFF_REC);
+  // Window-table records hold raw limbs (G1_TABLE_REC 7 pieces, G2_TABLE_REC 14: no unpacking); plain
+  // vectors are packed (6 / 12 pieces)
+  const bool limbs = G1 ? rec == G1_TABLE_REC : rec == G2_TABLE_REC;
   const int nq = limbs ? NQ : 2 * PW / 4;
   __shared__ uint4 pre[4][NQ][64];
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
@@ -733,14 +726,13 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
       a.y = F::unpack(w + PW);
     }
     if (e_cur & 0x80000000u) a = C::neg_affine(a);
-    const bool skip = limbs && (w[13] & AFF_IDENT);  // (a level record of the point at infinity)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS slot is read before it is refilled
     if (j + 1 < end) {
       issue(e_next);
       e_cur = e_next;
       e_next = (j + 2 < end) ? entry(j + 2) : 0u;
     }
-    if (!skip) acc = C::madd(acc, a);
+    acc = C::madd(acc, a);
   }
   if (started_here) store_point<C>(&bucket_sums[b], acc);
   else store_point<C>(&conts[seg], acc);
@@ -756,7 +748,7 @@ k_accumulate_g2d(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                  uint32_t* cont_bucket) {
   using F = Fp2Ops;
   constexpr int NW = sizeof(typename F::T) / 4;
-  const bool limbs = rec == G2_TABLE_REC || rec == G2_AFF_REC;
+  const bool limbs = rec == G2_TABLE_REC;
   const uint32_t E_lo = offsets[b_lo], E_hi = offsets[b_hi];
   const uint32_t seg = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t pos0 = seg * S;
@@ -833,24 +825,6 @@ void fit_segments_E(MsmShape& sh, size_t E) {
   const size_t slots = std::max<size_t>((size_t)(rounds * conc * fill) / 256 * 256, 256);
   size_t S = (E + slots - 1) / slots;
   sh.S = (int)std::min<size_t>(std::max<size_t>(S, min_s), (size_t)1 << 16);
-}
-
-// The batch-affine levels of this workspace's multiexp (msm.h): G1 window-table shapes on a
-// workspace with the context's level buffers; S = the XYZZ segment length over the last level.
-template <class C>
-AffinePlan affine_plan_for(const MsmWorkspace<C>& ws, size_t n, const MsmShape& sh) {
-  AffinePlan pl;
-  constexpr bool G1 = std::is_same<C, G1Ops>::value;
-  if (ws.aff && sh.rec == (int)(G1 ? G1_TABLE_REC : G2_TABLE_REC) && n > 0) {
-    pl = G1 ? affine_plan_g1(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves)
-            : affine_plan_g2(n * (size_t)sh.W, (size_t)sh.Wb * sh.NB, sh.halves);
-    if (pl.levels) {
-      MsmShape s2 = sh;
-      fit_segments_E<C>(s2, pl.Eb[pl.levels]);
-      pl.S = s2.S;
-    }
-  }
-  return pl;
 }
 
 template <class C>
@@ -969,11 +943,6 @@ void MsmWorkspace<C>::release() {
   if (seg_sum) hipFree(seg_sum);
   if (window_sums) hipFree(window_sums);
   if (host_window_sums) hipHostFree(host_window_sums);
-  for (uint32_t** p : {&aoff, &acnt, &ascan, &aspan}) {
-    if (*p) hipFree(*p);
-    *p = nullptr;
-  }
-  cap_anbt = 0;
   entries = counts = offsets = cursor = scan_scratch = nullptr;
   bucket_sums = conts = seg_weighted = seg_sum = window_sums = nullptr;
   host_window_sums = nullptr;
@@ -1002,26 +971,6 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
-    {
-      const AffinePlan pl = affine_plan_for<C>(ws, n, sh);
-      if (pl.levels) {  // batch-affine levels, then the XYZZ accumulation over the last level's records
-        // (the level buffers are the context's: held from their sizing to the last launch reading them)
-        std::lock_guard<std::mutex> lk(ws.aff->mu);
-        const uint32_t* fin = nullptr;
-        hipError_t e;
-        if constexpr (std::is_same<C, G1Ops>::value) e = affine_levels_g1(ws, st, d_bases, rec, pl, nbt, &fin);
-        else e = affine_levels_g2(ws, st, d_bases, rec, pl, nbt, &fin);
-        if (e != hipSuccess) return e;
-        const size_t fsegs = (pl.Eb[pl.levels] + pl.S - 1) / pl.S;
-        if ((e = ws.grow(0, 0, fsegs + 1, 0)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_accumulate_pf<C>, dim3(msm_blocks_for(fsegs, 256)), dim3(256), 0, st,
-                           (const uint32_t*)nullptr, ws.aoff + (size_t)(pl.levels - 1) * (nbt + 1), (uint32_t)nbt,
-                           fin, std::is_same<C, G1Ops>::value ? G1_AFF_REC : G2_AFF_REC, (uint32_t)pl.S, 0u,
-                           (uint32_t)nbt, ws.bucket_sums, ws.conts, ws.cont_bucket);
-        if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
-        return hipGetLastError();
-      }
-    }
     const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
     auto launch = [&](uint32_t lo, uint32_t hi) {
       if constexpr (!std::is_same<C, G1Ops>::value) {
@@ -1063,20 +1012,15 @@ struct SpanSrc {  // device-decided tails: k_max_span's words (null: the host de
 };
 
 // The sorted view the accumulation left for the reduction: the sort's counts/offsets and the
-// shape's S, or the last batch-affine level's (counts ceil(c / 2^levels), segments of plan.S).
+// shape's S.
 struct AccView {
   const uint32_t *counts, *offsets;
   uint32_t S;
   size_t E;  // upper bound of the accumulated records
-  const uint32_t* span_words;  // the last level's max-span words (null: the sort's)
+  const uint32_t* span_words;  // (null: the sort's, passed to msm_back)
 };
 template <class C>
 AccView acc_view(const MsmWorkspace<C>& ws, size_t n, const MsmShape& sh) {
-  const AffinePlan pl = affine_plan_for<C>(ws, n, sh);
-  if (pl.levels) {
-    const size_t nbt = (size_t)sh.Wb * sh.NB;
-    return AccView{ws.acnt, ws.aoff + (size_t)(pl.levels - 1) * (nbt + 1), (uint32_t)pl.S, pl.Eb[pl.levels], ws.aspan};
-  }
   return AccView{ws.counts, ws.offsets, (uint32_t)sh.S, n * (size_t)sh.W, nullptr};
 }
 
@@ -1135,10 +1079,6 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
     return e ? (size_t)atol(e) : (size_t)8;
   }();
   const AccView v = acc_view<C>(ws, n, sh);
-  if (v.span_words) {  // batch-affine levels: the last level's spans, read on the device
-    max_span = -1;
-    d_span_words = v.span_words;
-  }
   const size_t segs = (v.E + v.S - 1) / v.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
   const bool fold = max_span >= 0 && span <= REDUCE_FOLD_SPAN;

@@ -1204,12 +1204,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // by the host's ~0.4 ms of H enqueueing (mode 1), and H's first kernels reach the device
   // before the first accumulation fills every CU (mode 3)
   if (h_mode == 4 && (s = enqueue_h(jev[33]))) return s;
-  // (off while batch-affine levels are enabled: the accumulations on both streams would share
-  // one set of level buffers, ctx->aff1, that only the main stream's order protects)
   static const bool first_own = [] {
     const char* e = getenv("BH_FIRST_ACC_STREAM");
-    auto on = [](const char* n) { const char* x = getenv(n); return x && atoi(x) != 0; };
-    return !(e && e[0] == '0') && !on("BH_AFFINE") && !on("BH_AFFINE_G1") && !on("BH_AFFINE_G2");
+    return !(e && e[0] == '0');
   }();
   if (nbig > 0) {
     // wait for the last pre-sort that is a real sort: a trailing copy of another multiexp's

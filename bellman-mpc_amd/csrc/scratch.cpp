@@ -82,8 +82,6 @@ bh_status scratch_report(bh_ctx* ctx, uint64_t out[10], std::string* worst) {
   msm_acc_kernels<G2Ops>(ks);
   msm_back_kernels<G1Ops>(ks);
   msm_back_kernels<G2Ops>(ks);
-  aff_kernels_g1(ks);
-  aff_kernels_g2(ks);
   ntt_kernels(ks);
   dist_kernels(ks);
   const uint64_t cus = (uint64_t)std::max(prop.multiProcessorCount, 1);
