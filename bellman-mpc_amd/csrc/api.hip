@@ -773,12 +773,16 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   // puts them at the default priority (A/B experiments)
   const char* pe = getenv("BH_SIDE_PRIORITY");
   const int side = (pe && pe[0] == '0') ? prio_lo : prio_hi;
-  // (A/B) BH_MAIN_PRIORITY=1: the main stream (the G1 accumulations) at high priority too;
-  // BH_H_PRIORITY=0: the H stream at the default priority
+  // The main stream (the G1 accumulations) at high priority too (BH_MAIN_PRIORITY=0: default
+  // priority, round 4): with the G2 accumulation on a high-priority stream, a G1 workgroup lost every
+  // dispatch race for the register room beside a G2 wave to the sorts' and H's; round-5 rehearsal
+  // with the distributed H unmasked (below): N = 8 10.09-10.11 -> 9.61-9.66 ms per rank, N = 2
+  // 31.4-31.5 -> 31.0-31.1, N = 1 within noise (profiles/r05_ab_sched_N1_2_8.txt).
+  // BH_H_PRIORITY=0 (A/B): the H stream at the default priority.
   const char* me = getenv("BH_MAIN_PRIORITY");
   const char* he = getenv("BH_H_PRIORITY");
   const int hprio = (he && he[0] == '0') ? prio_lo : side;
-  if (me && me[0] == '1') {
+  if (!(me && me[0] == '0')) {
     (void)hipStreamDestroy(c->stream);
     if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
       release_mask(c); delete c;
@@ -831,11 +835,13 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
       *sp = m;
     }
   }
-  // The distributed H block (N >= 2 ranks) on half the CUs: its passes, all-to-alls and DFTs then
-  // leave the other half to the accumulations instead of taking every CU as their waves retire
-  // (N = 8 rehearsal: 10.88 -> 10.54 ms per rank; 64 or 192 CUs, or the sorts masked too, were
-  // no better: profiles/r03_ab_rehearsal_*).  Replicated H (one GPU) keeps the unmasked stream4.
-  if (masked("BH_DIST_H_CUS", &c->stream4d, ncu / 2) < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
+  // BH_DIST_H_CUS = k (A/B): the distributed H block (N >= 2 ranks) on a CU-masked stream of k CUs.
+  // Round 3 measured half the CUs better (N = 8: 10.88 -> 10.54 ms per rank) when the accumulations'
+  // stream had the default priority; a masked stream cannot be given high priority
+  // (hipExtStreamCreateWithCUMask), and with every prover stream at high priority (above) the
+  // unmasked H stream4 wins (round 5: N = 8 9.61-9.66 vs 10.09-10.11 ms with half the CUs, N = 2
+  // 31.0-31.1 vs 31.4-31.5; profiles/r05_ab_sched_N1_2_8.txt).  Default: 0, stream4.
+  if (masked("BH_DIST_H_CUS", &c->stream4d, 0) < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
