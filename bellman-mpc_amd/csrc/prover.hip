@@ -1204,6 +1204,16 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // by the host's ~0.4 ms of H enqueueing (mode 1), and H's first kernels reach the device
   // before the first accumulation fills every CU (mode 3)
   if (h_mode == 4 && (s = enqueue_h(jev[33]))) return s;
+  // 6 = enqueued there too, but starting on the device only once the first real sort is done:
+  // H's NTT passes fill every SIMD's register file (4 waves x 128 VGPRs) and LDS, so beside them
+  // the first sort's workgroups only got slots when H reached its first exchange (round-5 traces:
+  // the first k_part_count started 0.4 ms (N = 8) and 1.27 ms (N = 2) after the density maps)
+  if (h_mode == 6) {
+    int first_sort = -1;
+    for (int r = 0; r < pre_sorts && first_sort < 0; r++)
+      if (sorted_from[sorder[r]] == sorder[r]) first_sort = sorder[r];
+    if ((s = enqueue_h(first_sort >= 0 ? jev[16 + first_sort] : jev[33]))) return s;
+  }
   static const bool first_own = [] {
     const char* e = getenv("BH_FIRST_ACC_STREAM");
     return !(e && e[0] == '0');
