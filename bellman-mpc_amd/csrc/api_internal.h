@@ -218,6 +218,11 @@ struct bh_witness {
   size_t a_aux_total = 0, b_in_total = 0, b_aux_total = 0;
   // set bits before word k of each density map (k = 0..words): base index of a scalar shard
   std::vector<size_t> a_aux_prefix, b_aux_prefix;
+  // the density index maps (a_aux | b_input | b_aux: base index or -1 per scalar), built once at
+  // bh_witness_upload: a function of the density words only (the prover builds them per proof for
+  // bh_prove's per-call witness)
+  bh::DevBuf idx3;
+  bool idx_ready = false;
   // raw = true: abc/inputs/aux hold the caller's bls12_381 Montgomery words, not yet converted
   // (bh_prove's asynchronous upload; the prover converts on its own streams)
   bool raw = false;

@@ -206,6 +206,25 @@ bh_status witness_device_impl(bh_ctx* ctx, bh_witness* w, const uint64_t* a, con
   return BH_OK;
 }
 
+// the density index maps of a device-resident witness, once (density_index: a base index per
+// set bit, -1 per clear one), stream-ordered on st after the density words' upload
+bh_status witness_index_maps(bh_ctx* ctx, bh_witness* w, hipStream_t st) {
+  const size_t ni = w->num_inputs, na = w->num_aux;
+  const size_t maxn = std::max({w->m, ni, na, (size_t)1});
+  BH_TRY_HIP(w->idx3.alloc((2 * na + ni + 1) * 4));
+  BH_TRY_HIP(ctx->dtmp.alloc((maxn / 64 + 2) * 4));
+  BH_TRY_HIP(ctx->dscan.alloc(scan_scratch_words(maxn / 64 + 2) * 4 + 64));
+  const uint64_t* dens = w->dens.as<uint64_t>();
+  int32_t* ia = w->idx3.as<int32_t>();
+  if (na) BH_TRY_HIP(density_index(dens, na, (uint32_t)ni, ia, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), st));
+  if (ni) BH_TRY_HIP(density_index(dens + w->a_aux_words, ni, 0, ia + na, ctx->dtmp.as<uint32_t>(),
+                                   ctx->dscan.as<uint32_t>(), st));
+  if (na) BH_TRY_HIP(density_index(dens + w->a_aux_words + w->b_in_words, na, (uint32_t)w->b_in_total, ia + na + ni,
+                                   ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), st));
+  w->idx_ready = true;
+  return BH_OK;
+}
+
 // always leaves `up` in a final stage (2, or -1 with the status) so that no waiter hangs
 bh_status witness_device(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint64_t* b, const uint64_t* c,
                          const uint64_t* inputs, const uint64_t* aux, hipStream_t st, UploadSync* up) {
@@ -295,6 +314,7 @@ bh_status bh_witness_upload(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, c
                              b_aux_density);
   if (s) return s;
   if ((s = witness_device(ctx, w.get(), a, b, c, inputs, aux, ctx->h2d, nullptr))) return s;
+  if ((s = witness_index_maps(ctx, w.get(), ctx->h2d))) return s;
   BH_TRY_HIP(hipStreamSynchronize(ctx->h2d));
   *out = w.release();
   return BH_OK;
@@ -787,8 +807,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
 
   // ---- the 8 multiexps (prover.rs:233-307)
-  BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
-  int32_t* idx_aaux = ctx->idx3.as<int32_t>();
+  // (a resident witness carries its maps from bh_witness_upload; bh_prove's is rebuilt per call)
+  if (!w->idx_ready) BH_TRY_HIP(ctx->idx3.alloc((2 * na + ni + 1) * 4));
+  int32_t* idx_aaux = w->idx_ready ? const_cast<int32_t*>(w->idx3.as<int32_t>()) : ctx->idx3.as<int32_t>();
   int32_t* idx_bin = idx_aaux + na;
   int32_t* idx_baux = idx_bin + ni;
   // distributed H: this rank ends with its own share of h (dist_h.h), no range split
@@ -855,10 +876,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if (na) BH_TRY_HIP(scalars_prepare(ax, ax, na, 1, 0, sS));
     }
   }
-  if (na) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
+  if (na && !w->idx_ready) BH_TRY_HIP(density_index(d_a_aux, na, (uint32_t)ni, idx_aaux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
-  if (ni) BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), sS));
-  if (na) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx_baux, ctx->dtmp.as<uint32_t>(),
+  if (ni && !w->idx_ready)
+    BH_TRY_HIP(density_index(d_b_in, ni, 0, idx_bin, ctx->dtmp.as<uint32_t>(), ctx->dscan.as<uint32_t>(), sS));
+  if (na && !w->idx_ready) BH_TRY_HIP(density_index(d_b_aux, na, (uint32_t)w->b_in_total, idx_baux, ctx->dtmp.as<uint32_t>(),
                                    ctx->dscan.as<uint32_t>(), sS));
   MsmShape shapes[8];
   bool use_table[8] = {false};
