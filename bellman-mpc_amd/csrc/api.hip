@@ -788,6 +788,15 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
       release_mask(c); delete c;
       return BH_ERR_HIP;
     }
+    // ... and so must the host -> device copy stream be: with every compute queue at high priority,
+    // a default-priority queue's packets (the copies' completion markers the staging ring waits on)
+    // went unprocessed while the accumulations kept dispatching -- the drop-in's b and c landed at
+    // 33 and 45 ms instead of 7 and 10 (round-5 validation run)
+    (void)hipStreamDestroy(c->h2d);
+    if (hipStreamCreateWithPriority(&c->h2d, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+      release_mask(c); delete c;
+      return BH_ERR_HIP;
+    }
   }
   if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
@@ -1292,7 +1301,7 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
         int lo = 0, hi = 0;
         BH_TRY_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         BH_TRY_HIP(hipStreamCreateWithPriority(&bg.st, hipStreamNonBlocking, hi));
-        BH_TRY_HIP(hipStreamCreateWithFlags(&bg.cst, hipStreamNonBlocking));
+        BH_TRY_HIP(hipStreamCreateWithPriority(&bg.cst, hipStreamNonBlocking, hi));  // (as ctx->h2d)
         for (auto& e : bg.vec) BH_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         BH_TRY_HIP(bg.ring.init());
         bg.pool.reset(new HostPool(3));
