@@ -329,7 +329,12 @@ Jac<Fp> combine_g1(const XYZZ<G1F>* ws, const MsmShape& sh) {
   if (shift >= 0) {
     Jac<Fp> z = g1_from_xyzz(ws[1]);
     for (int k = 0; k < shift; k++) z = jac_dbl(z);
-    return jac_add(g1_from_xyzz(ws[0]), z);
+    z = jac_add(g1_from_xyzz(ws[0]), z);
+    if (sh.bucket_shard() && sh.bk_lo) {  // + bk_lo * (plain sum of the range's buckets)
+      const uint64_t k[1] = {sh.bk_lo};
+      z = jac_add(z, jac_mul(g1_from_xyzz(ws[2]), k, 1));
+    }
+    return z;
   }
   Jac<Fp> acc = jac_identity<Fp>();
   for (int w = sh.Wb - 1; w >= 0; w--) {
@@ -359,7 +364,12 @@ Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh) {
   if (shift >= 0) {
     Jac<bh::Fp2> z = g2_from_xyzz(ws[1]);
     for (int k = 0; k < shift; k++) z = jac_dbl(z);
-    return jac_add(g2_from_xyzz(ws[0]), z);
+    z = jac_add(g2_from_xyzz(ws[0]), z);
+    if (sh.bucket_shard() && sh.bk_lo) {  // + bk_lo * (plain sum of the range's buckets)
+      const uint64_t k[1] = {sh.bk_lo};
+      z = jac_add(z, jac_mul(g2_from_xyzz(ws[2]), k, 1));
+    }
+    return z;
   }
   Jac<bh::Fp2> acc = jac_identity<bh::Fp2>();
   for (int w = sh.Wb - 1; w >= 0; w--) {

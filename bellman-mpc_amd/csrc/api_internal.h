@@ -249,6 +249,9 @@ struct bh_ctx {
   bh::DistH* dist = nullptr;       // prover: this rank's distributed-H state (bh_prove_witness_partial_comm)
   int window_override = 0;
   int tables = 1;  // 1: the prover builds and uses SRS window tables (bh_ctx_set_tables)
+  // contexts of this device running ranks of one proof side by side (the virtual ranks of
+  // bh_prove_witness_partials_local): bucket shards weigh their workspaces by it
+  int co_ranks = 1;
   bh::MsmWorkspace<G1Ops> g1ws;
   bh::MsmWorkspace<G2Ops> g2ws;
   // one workspace per prover multiexp (result slot order), so that sorts, accumulations and

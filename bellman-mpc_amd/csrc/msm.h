@@ -30,7 +30,20 @@ struct MsmShape {
   // (the prover's last multiexp, msm_back); L2 = buckets per reduction thread of the upper half
   int halves = 0;
   int L2 = 0;
+  // Bucket shard (Wb == 1 only; bk_hi > bk_lo): only the digits whose bucket lies in
+  // [bk_lo, bk_hi) are sorted, accumulated and reduced -- one rank's part of a multiexp split
+  // across ranks by bucket range (every rank reads all scalars, the ranks' parts sum to the
+  // multiexp).  Both bounds are multiples of BUCKET_SHARD_GRANULE; the device returns three points
+  // (reduce_split_shift below).  0, 0: every bucket.
+  uint32_t bk_lo = 0, bk_hi = 0;
+  bool bucket_shard() const { return bk_hi > bk_lo; }
+  uint32_t red_lo() const { return bucket_shard() ? bk_lo : 0u; }
+  uint32_t red_nb() const { return bucket_shard() ? bk_hi - bk_lo : (uint32_t)NB; }
 };
+// a bucket shard's bounds are multiples of this: every partition of the digit sort (<= 128
+// buckets at the table window sizes) lies in one rank's range, and the range is a whole number
+// of k_reduce_blocks blocks (L * BT divides it: L <= 4 for G1's 256 threads, <= 8 for G2's 128)
+constexpr uint32_t BUCKET_SHARD_GRANULE = 1024;
 MsmShape msm_shape(size_t n, int c_override);
 // shape for a window table: c from the cost model n*ceil(256/c) + ~6.5 * 2^(c-1)
 int msm_table_c(size_t n);
@@ -58,7 +71,21 @@ inline int reduce_shift_for(uint32_t nbr, uint32_t L, bool g2) {
   return reduce_lg2(L) + reduce_lg2(reduce_threads_for(nbr, L, g2));
 }
 inline int reduce_split_shift(const MsmShape& sh, bool g2) {
-  return sh.Wb == 1 ? reduce_shift_for((uint32_t)sh.NB, (uint32_t)sh.L, g2) : -1;
+  return sh.Wb == 1 ? reduce_shift_for(sh.red_nb(), (uint32_t)sh.L, g2) : -1;
+}
+// A bucket shard's device result is out[0] + 2^reduce_split_shift * out[1] + bk_lo * out[2]
+// (combine_g1 / combine_g2; out[2] = the plain sum of the range's buckets, each of which holds
+// digit bk_lo more than its position in the range).
+// Level-2 geometry of the bucket reduction over nblk level-1 blocks: BT2 threads (a power of two)
+// of Lb blocks each (a power of two), BT2 * Lb >= nblk (blocks past nblk read as identities)
+inline void reduce_level2(uint32_t nblk, bool g2, uint32_t* BT2, uint32_t* Lb) {
+  const uint32_t bmax = g2 ? 128u : 256u;
+  uint32_t lb = 1;
+  while ((size_t)bmax * lb < nblk) lb <<= 1;
+  uint32_t t = 1;
+  while ((size_t)t * lb < nblk) t <<= 1;
+  *BT2 = t;
+  *Lb = lb;
 }
 // halves: out[0..3) is the lower half [0, NB/2): out[0] + 2^shift_lo * out[1]; out[3..6) the
 // upper half, reduced as a window of its own: out[3] + 2^shift_hi * out[4] + (NB/2) * out[5]
@@ -106,6 +133,8 @@ hipError_t msm_window_sums(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* 
 // set sh.S for curve C's accumulation kernel on the current device (see msm_impl.cuh)
 template <class C>
 void fit_segments(MsmShape& sh, size_t n);
+template <class C>
+void fit_segments_E(MsmShape& sh, size_t E);  // the same for E expected entries
 template <class C>
 hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
                     uint32_t base_offset, const MsmShape& sh);

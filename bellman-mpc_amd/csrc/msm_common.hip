@@ -35,8 +35,19 @@ static inline unsigned blocks_for(size_t n, unsigned bs) { return (unsigned)((n 
 
 // ----------------------------------------------------------------- scans
 // exclusive scan of uint32 (in place allowed), recursive over tiles of 1024
-__global__ void __launch_bounds__(256) k_scan_tile(const uint32_t* in, uint32_t* out, uint32_t* tile_sums, size_t n) {
+// dn (optional): a device word bounding the scan to its first *dn + 1 elements (tiles past it
+// exit; their sums read 0), for scans sized by a device-side count (derive_sorted)
+__device__ __forceinline__ size_t scan_len(size_t n, const uint32_t* dn) {
+  return dn ? min(n, (size_t)*dn + 1) : n;
+}
+__global__ void __launch_bounds__(256) k_scan_tile(const uint32_t* in, uint32_t* out, uint32_t* tile_sums, size_t n,
+                                                   const uint32_t* dn) {
   __shared__ uint32_t s[256];
+  n = scan_len(n, dn);
+  if ((size_t)blockIdx.x * 1024 >= n) {
+    if (threadIdx.x == 0 && tile_sums) tile_sums[blockIdx.x] = 0;
+    return;
+  }
   const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x * 4;
   uint32_t v[4];
   uint32_t local = 0;
@@ -62,9 +73,9 @@ __global__ void __launch_bounds__(256) k_scan_tile(const uint32_t* in, uint32_t*
   if (threadIdx.x == 255 && tile_sums) tile_sums[blockIdx.x] = s[255];
 }
 
-__global__ void k_scan_add(uint32_t* out, const uint32_t* tile_prefix, size_t n) {
+__global__ void k_scan_add(uint32_t* out, const uint32_t* tile_prefix, size_t n, const uint32_t* dn) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] += tile_prefix[i >> 10];
+  if (i < scan_len(n, dn)) out[i] += tile_prefix[i >> 10];
 }
 
 // scratch must hold scan_scratch_words(n) words
@@ -74,17 +85,22 @@ size_t scan_scratch_words(size_t n) {
   return tiles + scan_scratch_words(tiles);
 }
 
-void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st) {
+static void exclusive_scan_b(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st,
+                             const uint32_t* dn) {
   size_t tiles = (n + 1023) / 1024;
   if (tiles == 0) return;
   if (tiles == 1) {
-    hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, st, in, out, (uint32_t*)nullptr, n);
+    hipLaunchKernelGGL(k_scan_tile, dim3(1), dim3(256), 0, st, in, out, (uint32_t*)nullptr, n, dn);
     return;
   }
   uint32_t* sums = scratch;
-  hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)tiles), dim3(256), 0, st, in, out, sums, n);
-  exclusive_scan(sums, sums, tiles, scratch + tiles, st);
-  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, sums, n);
+  hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)tiles), dim3(256), 0, st, in, out, sums, n, dn);
+  exclusive_scan_b(sums, sums, tiles, scratch + tiles, st, nullptr);  // (the tile sums past dn are 0)
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, sums, n, dn);
+}
+
+void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, uint32_t* scratch, hipStream_t st) {
+  exclusive_scan_b(in, out, n, scratch, st, nullptr);
 }
 
 // ----------------------------------------------------------------- scalars
@@ -301,9 +317,11 @@ MsmShape msm_shape_table(size_t n, int c) {
 // array plus counts[gb] / offsets[gb] for every bucket of the partition.
 static constexpr int PT_TILE = 4096;  // scalars per tile
 
+// [plo, phi): the partitions a bucket shard keeps (MsmShape::bk_lo); digits outside are skipped by
+// both passes, so the scan leaves their partitions empty and k_part_sort writes zero counts there
 __global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, size_t n, const int32_t* idx,
                                                     DigitCfg cfg, int lo_bits, uint32_t P, uint32_t ntiles,
-                                                    uint32_t* tilecounts) {
+                                                    uint32_t plo, uint32_t phi, uint32_t* tilecounts) {
   extern __shared__ uint32_t hist[];
   for (uint32_t i = threadIdx.x; i < P; i += 256) hist[i] = 0;
   __syncthreads();
@@ -316,7 +334,10 @@ __global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, siz
     uint32_t carry = 0;
     for (int w = 0; w < cfg.W; w++) {
       const int d = digit_at(sc, w, cfg.c, carry);
-      if (d != 0) atomicAdd(&hist[digit_bucket(cfg, w, d) >> lo_bits], 1u);
+      if (d != 0) {
+        const uint32_t p = digit_bucket(cfg, w, d) >> lo_bits;
+        if (p - plo < phi - plo) atomicAdd(&hist[p], 1u);
+      }
     }
   }
   __syncthreads();
@@ -327,7 +348,8 @@ __global__ void __launch_bounds__(256) k_part_count(const uint32_t* scalars, siz
 
 __global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, size_t n, const int32_t* idx,
                                                       uint32_t base_offset, DigitCfg cfg, int lo_bits, uint32_t P,
-                                                      uint32_t ntiles, const uint32_t* offs, uint2* recs) {
+                                                      uint32_t ntiles, uint32_t plo, uint32_t phi,
+                                                      const uint32_t* offs, uint2* recs) {
   extern __shared__ uint32_t cur[];
   for (uint32_t p = threadIdx.x; p < P; p += 256) cur[p] = offs[(size_t)p * ntiles + blockIdx.x];
   __syncthreads();
@@ -350,6 +372,7 @@ __global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, s
       const int d = digit_at(sc, w, cfg.c, carry);
       if (d != 0) {
         const uint32_t gb = digit_bucket(cfg, w, d);
+        if ((gb >> lo_bits) - plo >= phi - plo) continue;
         const uint32_t pos = atomicAdd(&cur[gb >> lo_bits], 1u);
         recs[pos] = make_uint2(digit_entry(cfg, base, w, d), gb & lo_mask);
       }
@@ -422,9 +445,10 @@ __global__ void __launch_bounds__(256) k_derive_mark(const uint32_t* src_entries
                                                      int pre, uint32_t W, uint32_t src_off, const int32_t* idx,
                                                      uint32_t* mark) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j > Emax) return;
+  const uint32_t E = *src_E;
+  if (j > Emax || j > E) return;  // (the scan reads marks 0 .. src_E only)
   uint32_t ne;
-  mark[j] = (j < *src_E && derive_keep(src_entries[j], pre, W, src_off, idx, &ne)) ? 1u : 0u;
+  mark[j] = (j < E && derive_keep(src_entries[j], pre, W, src_off, idx, &ne)) ? 1u : 0u;
 }
 
 __global__ void __launch_bounds__(256) k_derive_write(const uint32_t* src_entries, const uint32_t* src_E, int pre,
@@ -453,7 +477,8 @@ hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offset
   const uint32_t* src_E = src_offsets + nbt;
   hipLaunchKernelGGL(k_derive_mark, dim3(blocks_for(Emax + 1, 256)), dim3(256), 0, st, src_entries, src_E, Emax, pre, W,
                      src_off, idx, pos);
-  exclusive_scan(pos, pos, Emax + 1, scan_scratch, st);
+  // positions 0 .. src_E only: with a bucket shard the source holds ~1/N of the Emax records
+  exclusive_scan_b(pos, pos, Emax + 1, scan_scratch, st, src_E);
   hipLaunchKernelGGL(k_derive_write, dim3(blocks_for(Emax, 256)), dim3(256), 0, st, src_entries, src_E, pre, W, src_off,
                      idx, pos, dst_entries);
   hipLaunchKernelGGL(k_derive_offsets, dim3(blocks_for(nbt + 1, 256)), dim3(256), 0, st, src_offsets, nbt, pos,
@@ -493,10 +518,15 @@ hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_id
     hipMemsetAsync(offsets, 0, (nbt + 1) * 4, st);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_part_count, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, cfg, lo, P, nt, tilecounts);
+  // a bucket shard keeps the partitions of [bk_lo, bk_hi) (multiples of BUCKET_SHARD_GRANULE, so
+  // of the partition width 2^lo)
+  const uint32_t plo = sh.bucket_shard() ? sh.bk_lo >> lo : 0u;
+  const uint32_t phi = sh.bucket_shard() ? sh.bk_hi >> lo : P;
+  hipLaunchKernelGGL(k_part_count, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, cfg, lo, P, nt, plo, phi,
+                     tilecounts);
   exclusive_scan(tilecounts, tilecounts, tw, tscan_scratch, st);
   hipLaunchKernelGGL(k_part_scatter, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, base_offset, cfg, lo, P,
-                     nt, tilecounts, recs);
+                     nt, plo, phi, tilecounts, recs);
   hipLaunchKernelGGL(k_part_sort, dim3(P), dim3(256), 0, st, recs, tilecounts, nt, P, lo, (uint32_t)nbt, entries,
                      counts, offsets);
   return hipGetLastError();

@@ -11,6 +11,7 @@
 namespace bh {
 template struct MsmWorkspace<G2Ops>;
 template void fit_segments<G2Ops>(MsmShape&, size_t);
+template void fit_segments_E<G2Ops>(MsmShape&, size_t);
 template hipError_t msm_sort<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const int32_t*,
                                      uint32_t, const MsmShape&);
 template hipError_t msm_accumulate<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const MsmShape&,

@@ -10,6 +10,7 @@ namespace bh {
 // instantiated in msm_g2_acc.hip (the accumulation kernels compile there, in parallel)
 extern template struct MsmWorkspace<G2Ops>;
 extern template void fit_segments<G2Ops>(MsmShape&, size_t);
+extern template void fit_segments_E<G2Ops>(MsmShape&, size_t);
 extern template hipError_t msm_sort<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t, const int32_t*,
                                             uint32_t, const MsmShape&);
 extern template hipError_t msm_accumulate<G2Ops>(MsmWorkspace<G2Ops>&, hipStream_t, const uint32_t*, size_t,

@@ -388,13 +388,15 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const t
   const uint32_t i = threadIdx.x, w = blockIdx.x;
   const size_t base = (size_t)w * nblk + (size_t)i * Lb;
   typename C::P run = C::identity(), acc = C::identity(), p = C::identity();
-  // per block k = Lb-1 .. 0:  acc += run;  run += S_k;  p += Y_k
+  // per block k = Lb-1 .. 0:  acc += run;  run += S_k;  p += Y_k  (blocks past nblk: identities,
+  // reduce_level2)
   for (uint32_t it = 0; it < 3 * Lb; it++) {
     const uint32_t k = Lb - 1 - it / 3, op = it % 3;
+    const bool in = i * Lb + k < nblk;
     typename C::P a, b;
     if (op == 0) { a = acc; b = run; }
-    else if (op == 1) { a = run; b = load_point<C>(&Ssum[base + k]); }
-    else { a = p; b = load_point<C>(&Y[base + k]); }
+    else if (op == 1) { a = run; b = in ? load_point<C>(&Ssum[base + k]) : C::identity(); }
+    else { a = p; b = in ? load_point<C>(&Y[base + k]) : C::identity(); }
     const typename C::P r = C::add(a, b);
     if (op == 0) acc = r;
     else if (op == 1) run = r;
@@ -1055,8 +1057,8 @@ static void reduce_range(MsmWorkspace<C>& ws, const AccView& v, hipStream_t st, 
   const uint32_t T = nbr / L;
   const uint32_t BT = reduce_threads_for(nbr, L, G2);
   const uint32_t nblk = T / BT;
-  const uint32_t BT2 = std::min(nblk, G2 ? 128u : 256u);
-  const uint32_t Lb = nblk / BT2;
+  uint32_t BT2, Lb;
+  reduce_level2(nblk, G2, &BT2, &Lb);
   const int split = sh.Wb == 1 ? 1 : 0;
   hipLaunchKernelGGL(k_reduce_blocks<C>, dim3((unsigned)(sh.Wb * nblk)), dim3(BT), BT * sizeof(typename C::P), st,
                      v.counts, v.offsets, ws.bucket_sums, ws.conts, v.S, b0, (uint32_t)sh.NB, L, reduce_lg2(L), nblk,
@@ -1099,9 +1101,10 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
     hipMemcpyAsync(host_out, ws.window_sums, 6 * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
     return hipGetLastError();
   }
-  reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, 0, (uint32_t)sh.NB, (uint32_t)sh.L, 0, ws.window_sums, dev);
-  hipMemcpyAsync(host_out, ws.window_sums, (sh.Wb == 1 ? 2 : sh.Wb) * sizeof(typename C::P), hipMemcpyDeviceToHost,
-                 st);
+  reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, sh.red_lo(), sh.red_nb(), (uint32_t)sh.L, 0, ws.window_sums,
+                  dev);
+  const int outs = sh.bucket_shard() ? 3 : (sh.Wb == 1 ? 2 : sh.Wb);
+  hipMemcpyAsync(host_out, ws.window_sums, outs * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
   return hipGetLastError();
 }
 

@@ -354,6 +354,85 @@ int table_c_for(size_t used_per_shard) {
   return used_per_shard >= TABLE_MIN_USED ? msm_table_c(used_per_shard) : 0;
 }
 
+// ---- Bucket shards.  With N > 1 ranks a table multiexp (one shared set of 2^(c-1) buckets)
+// is split by BUCKET range instead of scalar range: every rank reads all the scalars, keeps the
+// digits that fall in its range of buckets, accumulates and reduces only those, and the ranks'
+// parts sum to the multiexp like scalar shards do (bh_proof_from_partials).  Against a scalar
+// shard of n/N points, which needs its own smaller window (c = 16 at 2^19 points: 16 windows
+// against 13) and still reduces a whole bucket set of its own, each rank keeps one GPU's c = 20
+// and 1/N of its bucket reduction.  The ranges come from the digit distribution of uniformly
+// distributed scalars (bucket_cdf); a skewed witness (e.g. many small values) stays correct, its
+// ranks just do unequal work.  Measured in the one-GPU rehearsal at 2^22 (round 5,
+// profiles/r05_ab_bucket_shards.txt) it is no faster than scalar shards: each rank's G1
+// accumulations take ~12 % less time, but every rank sorts all the scalars (8x the partition
+// scan), and its bucket range holds as many continuation partials per bucket as a c = 16 shard's
+// buckets do, so the reductions do not shrink.  Off by default; BH_SHARD_BUCKETS=1 (read per
+// proof, on every rank alike) selects it.
+bool bucket_shards_on() {
+  const char* e = getenv("BH_SHARD_BUCKETS");
+  return e && e[0] == '1';
+}
+
+// Expected digits per scalar in buckets [0, b) of a shared-bucket table of W c-bit signed
+// windows (digit_at): the W - 1 lower windows spread |d| in [1, 2^(c-1)] evenly over the
+// NB = 2^(c-1) buckets; the top window holds t + carry with t <= T = (r - 1) >> (c * (W - 1))
+// (r: the Fr modulus, 0x73eda753299d7d48... in its top 64 bits), so its digits fill buckets
+// [0, T + 1) evenly.
+double bucket_cdf(int c, int W, double b) {
+  const double NB = (double)((size_t)1 << (c - 1));
+  const int top_shift = c * (W - 1);
+  double T1 = NB;  // (a top window below bit 192: treated like the others)
+  if (top_shift >= 192 && top_shift < 256) T1 = (double)(0x73eda753299d7d48ull >> (top_shift - 192)) + 1.0;
+  if (T1 > NB) T1 = NB;
+  return (W - 1) * b / NB + std::min(b, T1) / T1;
+}
+
+// Bucket shards for a proof with na aux scalars on N ranks, co_ranks of them side by side on
+// each device?  The same answer on every rank (a function of the shape only): every rank sorts all
+// na scalars of the four aux multiexps, so its workspaces (entries + partition records, 12 B per
+// digit, and the continuation partials) do not shrink with N -- ~5 GB per rank at 2^22.  Scalar
+// shards when co_ranks of them would take over a quarter of the device (8 virtual ranks at 2^24).
+bool bucket_shards_use(int device, size_t na, size_t nshards, int co_ranks) {
+  if (nshards < 2 || !bucket_shards_on()) return false;
+  size_t total = 0;
+  if (hipDeviceTotalMem(&total, device) != hipSuccess || total == 0) return false;
+  const double ws = 4.0 * (double)na * 16.0 * 12.0 * 1.6;  // (16: the most windows of a table size)
+  return (double)std::max(co_ranks, 1) * ws <= (double)total / 4.0;
+}
+
+// Rank `shard` of N: its bucket range [lo, hi), granule-aligned, balancing the expected
+// accumulation (used * bucket_cdf) plus the reduction (BH_SHARD_BUCKET_W = 3 additions per
+// bucket).  False when the bucket set is too small to give every rank several granules.
+bool bucket_shard_range(int c, size_t used, size_t shard, size_t N, uint32_t* lo, uint32_t* hi) {
+  const int W = (256 + c - 1) / c;
+  const uint32_t NB = 1u << (c - 1);
+  const uint32_t G = std::max<uint32_t>(BUCKET_SHARD_GRANULE, NB >> 12);  // (sort partition width)
+  if ((size_t)NB < 4 * N * G) return false;
+  const double kw = [] {
+    const char* e = getenv("BH_SHARD_BUCKET_W");
+    return e ? atof(e) : 3.0;
+  }();
+  auto cost = [&](double b) { return (double)used * bucket_cdf(c, W, b) + kw * b; };
+  const double total = cost(NB);
+  auto bound = [&](size_t k) -> uint32_t {
+    if (k == 0) return 0;
+    if (k >= N) return NB;
+    const double target = total * (double)k / (double)N;
+    double a = 0, z = NB;
+    for (int it = 0; it < 64; it++) {
+      const double m = 0.5 * (a + z);
+      (cost(m) < target ? a : z) = m;
+    }
+    uint32_t g = (uint32_t)std::llround(a / G);
+    g = std::max<uint32_t>(g, (uint32_t)k);                      // every rank keeps >= one granule
+    g = std::min<uint32_t>(g, NB / G - (uint32_t)(N - k));
+    return g * G;
+  };
+  *lo = bound(shard);
+  *hi = bound(shard + 1);
+  return *hi > *lo;
+}
+
 // Window table of c-bit windows over the bases [lo, hi) of srs (a shard's slice, or the whole
 // vector): kept if the resident table already covers them at this c, else rebuilt for exactly
 // [lo, hi).  Skipped (plain windows, same results) when HBM is short -- reported once.
@@ -437,6 +516,7 @@ struct Job {
   size_t lo = 0, hi = 0;    // this shard's scalars
   size_t blo = 0, bhi = 0;  // the bases they consume
   int table_c = 0;          // window size of this job's table (0: plain windows)
+  uint32_t bk_lo = 0, bk_hi = 0;  // bucket shard (MsmShape::bk_lo): every scalar, these buckets
 };
 
 inline size_t dens_before(const Job& J, size_t i) {
@@ -620,11 +700,24 @@ bh_status plan_shard(bh_ctx* ctx, const bh_params* params_c, const bh_witness* w
   jobs[5] = mk(false, &params->a, inputs, ni, nullptr, ni, 2, nullptr, nullptr, 0);                   // a_inputs
   jobs[6] = mk(false, &params->b_g1, inputs, ni, idx_bin, w->b_in_total, 4, nullptr, nullptr, 0);     // b_g1_inputs
   jobs[7] = mk(true, &params->b_g2, inputs, ni, idx_bin, w->b_in_total, 0, nullptr, nullptr, 0);      // b_g2_inputs
+  // the large aux multiexps (b_g2_aux, b_g1_aux, l, a_aux) are bucket shards when N > 1
+  const bool bshard = tables && bucket_shards_use(ctx->device, na, nshards, ctx->co_ranks);
   for (int j = 0; j < 8; j++) {
     Job& J = jobs[j];
+    J.table_c = 0;
+    J.bk_lo = J.bk_hi = 0;
+    if (bshard && j <= 3 && !J.is_h && J.n && J.used >= TABLE_MIN_USED) {
+      const int c = table_c_for(J.used);
+      if (c && bucket_shard_range(c, J.used, shard, nshards, &J.bk_lo, &J.bk_hi)) {
+        J.lo = 0; J.hi = J.n;
+        J.blo = J.boff; J.bhi = J.boff + dens_before(J, J.n);
+        J.table_c = c;
+        continue;
+      }
+      J.bk_lo = J.bk_hi = 0;
+    }
     if (J.presharded) { J.lo = 0; J.hi = J.n; }
     else shard_range(J.n, shard, nshards, &J.lo, &J.hi);
-    J.table_c = 0;
     if (J.hi == J.lo) continue;
     const size_t used = (size_t)((unsigned __int128)J.used * (J.hi - J.lo) / std::max<size_t>(J.n, 1));
     if (J.idx && !J.prefix && J.presharded) {  // h share over the full vector: any base may be used
@@ -665,11 +758,15 @@ bool plan_needs_build(const bh_params* params, const Job jobs[8], const ShareGeo
 // Full-vector tables at the window size of one of nshards shards (bh_params_prepare): every
 // shard's slice is covered, so one device can run all N shards (rehearsal, partials_local).
 bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t na, size_t a_aux_used,
-                              size_t b_aux_used, size_t nshards) {
+                              size_t b_aux_used, size_t nshards, int co_ranks = 1) {
   if (!ctx->tables || ctx->window_override) return BH_OK;
   const size_t N = std::max<size_t>(nshards, 1);
   bh_status s;
-  auto full = [&](bh_srs* v, size_t used) { return ensure_table(ctx, v, table_c_for(used / N), 0, v->n); };
+  // bucket shards (plan_shard) keep one GPU's window size for the aux vectors
+  const size_t Naux = bucket_shards_use(ctx->device, na, N, co_ranks) ? 1 : N;
+  auto full = [&](bh_srs* v, size_t used) {
+    return ensure_table(ctx, v, table_c_for(used / (v == &params->h ? N : Naux)), 0, v->n);
+  };
   if ((s = full(&params->h, m - 1))) return s;
   if ((s = full(&params->l, na))) return s;
   if ((s = full(&params->a, a_aux_used))) return s;
@@ -892,11 +989,39 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (his[j] == los[j]) continue;
     const bh_srs* srs = jobs[j].srs;
     use_table[j] = jobs[j].table_c && srs->win_covers(jobs[j].table_c, jobs[j].blo, jobs[j].bhi);
+    if (jobs[j].bk_hi && !use_table[j]) {
+      // a bucket shard without its table (HBM short): rank 0 runs the whole multiexp with plain
+      // windows, the others nothing (the parts still sum to the multiexp)
+      jobs[j].bk_lo = jobs[j].bk_hi = 0;
+      if (shard != 0) {
+        his[j] = los[j];
+        continue;
+      }
+    }
     shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
                              : msm_shape(his[j] - los[j], ctx->window_override);
     if (use_table[j]) shapes[j].rec = srs->win_rec;
-    if (jobs[j].g2) fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
-    else fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
+    if (jobs[j].bk_hi) {
+      MsmShape& sh = shapes[j];
+      sh.bk_lo = jobs[j].bk_lo;
+      sh.bk_hi = jobs[j].bk_hi;
+      // reduction geometry: L * BT divides the granule (BUCKET_SHARD_GRANULE), and at least as many
+      // reduction threads as one GPU's whole bucket set gets (msm_shape_table: 16 384), since a
+      // shard's buckets hold as many continuation partials each (a round-5 rank of 8: G2 with 8 192
+      // threads was a 4.6 ms reduction at the end of the proof)
+      const uint32_t BT = reduce_block_max(jobs[j].g2);
+      while (sh.L > 1 && ((uint32_t)sh.L * BT > BUCKET_SHARD_GRANULE || sh.red_nb() / (uint32_t)sh.L < 16384u))
+        sh.L >>= 1;
+      // segments sized for the range's expected entries (the grid still covers every position)
+      const double f = bucket_cdf(sh.c, sh.W, sh.bk_hi) - bucket_cdf(sh.c, sh.W, sh.bk_lo);
+      const size_t E = std::max<size_t>((size_t)((double)jobs[j].used * f), 1);
+      if (jobs[j].g2) fit_segments_E<G2Ops>(sh, E);
+      else fit_segments_E<G1Ops>(sh, E);
+    } else if (jobs[j].g2) {
+      fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
+    } else {
+      fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
+    }
     if (jobs[j].table_c) n_large++;
     if (use_table[j]) n_table++;
   }
@@ -951,7 +1076,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   auto same_digits = [&](int i, int j) {
     const MsmShape &a = shapes[i], &b = shapes[j];
     return jobs[i].sc == jobs[j].sc && jobs[i].idx == jobs[j].idx && los[i] == los[j] && his[i] == his[j] &&
-           a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre;
+           a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre && a.bk_lo == b.bk_lo &&
+           a.bk_hi == b.bk_hi;
   };
   // ... and one over a sparser density map (a_aux, b_aux under l's dense one) compacts it
   static const bool derive_on = [] {  // BH_SORT_DERIVE=0: full sorts only (A/B experiments)
@@ -961,7 +1087,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   auto derivable = [&](int i, int j) {
     const MsmShape &a = shapes[i], &b = shapes[j];
     return derive_on && jobs[i].sc == jobs[j].sc && !jobs[i].idx && jobs[j].idx && !jobs[i].is_h && los[i] == los[j] &&
-           his[i] == his[j] && a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre;
+           his[i] == his[j] && a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre &&
+           a.bk_lo == b.bk_lo && a.bk_hi == b.bk_hi;
   };
   int sorted_from[8];
   for (int j = 0; j < 8; j++) sorted_from[j] = -1;
@@ -1130,9 +1257,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       const char* e = getenv("BH_LAST_HALVES");
       return e && e[0] == '1';
     }();
-    const bool halves = last_halves && sl.Wb == 1 && sl.NB >= 4096 && !serial;
+    const bool halves = last_halves && sl.Wb == 1 && sl.NB >= 4096 && !serial && !sl.bucket_shard();
     if (last_threads > 0) {
-      const int nb = halves ? sl.NB / 2 : sl.NB;
+      const int nb = halves ? sl.NB / 2 : (int)sl.red_nb();
       int L = sl.L;
       while (L > 1 && (size_t)sl.Wb * (size_t)(nb / L) < (size_t)last_threads) L >>= 1;
       if (halves) {
@@ -1725,13 +1852,14 @@ bh_status bh_prove_witness_partials_local(bh_ctx* ctx, const bh_params* params, 
   for (bh_ctx* v : ctxs) {
     v->tables = ctx->tables;
     v->window_override = ctx->window_override;
+    v->co_ranks = N;
   }
   // one Parameters for every rank: tables covering every shard (full vectors at the shard's
   // window size) are built once up front
   {
     std::unique_lock<std::shared_mutex> pwr(const_cast<bh_params*>(params)->mu);
     bh_status s = prepare_tables_full(ctx, const_cast<bh_params*>(params), w->m, w->num_aux, w->a_aux_total,
-                                      w->b_aux_total, nshards);
+                                      w->b_aux_total, nshards, N);
     if (s) return s;
   }
   std::vector<const bh_params*> ps(N, params);
