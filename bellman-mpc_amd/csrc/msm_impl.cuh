@@ -803,10 +803,16 @@ void fit_segments_E(MsmShape& sh, size_t E) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k, 256, 0) != hipSuccess || blocks < 1) blocks = 1;
     return (size_t)cus * (size_t)blocks * 256;
   }();
+  // 3 rounds (round 5; 4 before): same-box 2^22 bench 53.2-53.4 ms per proof against 54.6 with 4,
+  // 53.4-53.9 with 2, 58.5-59.4 with 1, and the rehearsal faster at N = 1, 2 and 8 too
+  // (profiles/r05_ab_acc_rounds.txt): fewer segments are fewer continuation partials and bucket
+  // stores, and with the G2 and G1 accumulations sharing the SIMDs a third round balances the
+  // finish well enough.  BH_ACC_ROUNDS (BH_ACC_ROUNDS_G1 / BH_ACC_ROUNDS_G2: one group only)
   static const size_t rounds = [] {
-    const char* e = getenv("BH_ACC_ROUNDS");
-    const int r = e ? atoi(e) : 4;
-    return (size_t)(r > 0 ? r : 4);
+    const char* e = getenv(std::is_same<C, G1Ops>::value ? "BH_ACC_ROUNDS_G1" : "BH_ACC_ROUNDS_G2");
+    if (!e) e = getenv("BH_ACC_ROUNDS");
+    const int r = e ? atoi(e) : 3;
+    return (size_t)(r > 0 ? r : 3);
   }();
   // BH_ACC_FILL: fraction of the resident capacity the accumulation occupies per round
   // (the rest stays free for the side streams' short kernels)

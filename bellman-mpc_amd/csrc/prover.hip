@@ -1273,12 +1273,12 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       sl.L2 = sl.L;
     }
     // BH_LAST_ACC_ROUNDS = r (A/B experiments): the last accumulation in r resident rounds instead
-    // of fit_segments' 4 (longer segments: fewer continuation partials for its tail to fold)
+    // of fit_segments' 3 (longer segments: fewer continuation partials for its tail to fold)
     static const int last_rounds = [] {
       const char* e = getenv("BH_LAST_ACC_ROUNDS");
       return e ? atoi(e) : 0;
     }();
-    if (last_rounds > 0 && last_rounds < 4) sl.S = std::min(sl.S * 4 / last_rounds, 1 << 16);
+    if (last_rounds > 0 && last_rounds < 3) sl.S = std::min(sl.S * 3 / last_rounds, 1 << 16);
   }
   // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it;
   // 1 = from the start, concurrent with everything (the default); 2 = after the first
