@@ -331,40 +331,6 @@ def test_window_tables_match_plain_windows(ctx, logc):
     assert bh.prove_witness(ctx, params, w, 27134, 17146) == plain
     parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, 2) for k in range(2))
     assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
-    # bucket shards: with every scalar equal, one rank's bucket range holds every entry
-    monkeypatch.setenv("BH_SHARD_BUCKETS", "1")
-    for n in (2, 8):
-        parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, n) for k in range(n))
-        assert bh.proof_from_partials(params.vk_bytes(), parts, n, 27134, 17146) == plain
-
-
-@pytest.mark.parametrize("nshards", [2, 3, 8])
-def test_bucket_shards_equal_single_proof(ctx, monkeypatch, nshards):
-    """BH_SHARD_BUCKETS=1 (prover.hip, bucket_shard_range): the large aux multiexps split across
-    ranks by bucket range -- every rank sorts all the scalars and keeps the digits of its own
-    granule-aligned range of the shared c-bit bucket set, and its reduction adds bk_lo times the
-    range's plain sum -- at 2^17 constraints (window tables in use).  The per-rank partials (one
-    context, rank after rank) and the virtual-rank run with the distributed H block both
-    recombine to the single-device proof."""
-    bh = _bh()
-    rounds = (1 << 16) - 1
-    params = bh.Parameters.chain(ctx, rounds)
-    w = bh.Witness.chain(ctx, rounds)
-    single = bh.prove_witness(ctx, params, w, 27134, 17146)
-    monkeypatch.setenv("BH_SHARD_BUCKETS", "1")
-    params.prepare(w, nshards)
-    parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, nshards) for k in range(nshards))
-    assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146) == single
-    if nshards & (nshards - 1) == 0:
-        parts = bh.prove_witness_partials_local(ctx, params, w, nshards)
-        assert bh.proof_from_partials(params.vk_bytes(), parts, nshards, 27134, 17146) == single
-    if logc == 22:
-        # the benchmark's own proof (C3) equals the oracle port's proof of the same CRS and
-        # witness, recorded in tests/golden/port_proofs.json by tools/cpu_baseline_full.py
-        # --fixture (prover.rs:315-349 output)
-        fx = _port_proof(22)
-        assert hashlib.sha256(params.write()).hexdigest() == fx["params_sha256"]
-        assert plain.hex() == fx["proof_port"]
 
 
 def test_checked_load_rejects_points_outside_subgroup(ctx):
