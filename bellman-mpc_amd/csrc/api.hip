@@ -542,6 +542,10 @@ bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
   d->lo_bits = (L + 1) / 2;
   bh_status s;
   if ((s = upload_split_table(ctx, d->coset_lo, d->coset_hi, g, d->minv, L, d->lo_bits))) return s;
+  {
+    DevBuf lo32;  // (identical to coset_lo)
+    if ((s = upload_split_table(ctx, lo32, d->coset_hi32, g, mul(d->minv, fr_small(32)), L, d->lo_bits))) return s;
+  }
   if ((s = upload_split_table(ctx, d->icoset_lo, d->icoset_hi, ginv, d->minv, L, d->lo_bits))) return s;
   if ((s = upload_split_table(ctx, d->gpow_lo, d->gpow_hi, g, Fr::one(), L, d->lo_bits))) return s;
   uint32_t cst[3 * 9];
@@ -654,15 +658,17 @@ static bh_status host_fft(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m, FftKind
 // untouched, no copy).  Without hout, on return d_abc's first m entries hold the h coefficients
 // in BIT-REVERSED order (device form); with hout, the last pass writes the m-1 canonical h
 // scalars in natural order to hout instead (truncation + to_le_bits fused).
-bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v) {
+bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v,
+                       bool raw_src) {
   const int L = D->L;
   const size_t m = (size_t)1 << L;
   // prover.rs:214-219: ifft (DIF, omega^-1) with m^-1 * g^i fused = ifft + distribute_powers(g);
   // then fft (DIT, bit-reversed -> natural) = coset_fft; c's storing pass computes
   // (a*b - c) / Z(g) into a (prover.rs:221-225: mul_assign, sub_assign, divide_by_z_on_coset)
   uint32_t* x = d_abc + (size_t)v * m * 8;
-  launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(), D->coset_hi.as<uint32_t>(),
-             D->lo_bits, st, src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
+  launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(),
+             (raw_src ? D->coset_hi32 : D->coset_hi).as<uint32_t>(), D->lo_bits, st,
+             src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
   NttEpilogue e;
   if (v == 2) {
     e.kind = NttEpilogue::AB_MINUS_C;
@@ -789,14 +795,20 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   // with the distributed H unmasked (below): N = 8 10.09-10.11 -> 9.61-9.66 ms per rank, N = 2
   // 31.4-31.5 -> 31.0-31.1, N = 1 within noise (profiles/r05_ab_sched_N1_2_8.txt).
   // BH_H_PRIORITY=0 (A/B): the H stream at the default priority.
+  // BH_ACC_PRIORITY=0 (A/B): both accumulation streams (main and the first accumulation's) at the
+  // default priority, below H, the sorts and the tails.
   const char* me = getenv("BH_MAIN_PRIORITY");
   const char* he = getenv("BH_H_PRIORITY");
+  const char* ae = getenv("BH_ACC_PRIORITY");
+  const bool acc_lo = ae && ae[0] == '0';
   const int hprio = (he && he[0] == '0') ? prio_lo : side;
   if (!(me && me[0] == '0')) {
-    (void)hipStreamDestroy(c->stream);
-    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-      release_mask(c); delete c;
-      return BH_ERR_HIP;
+    if (!acc_lo) {
+      (void)hipStreamDestroy(c->stream);
+      if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        release_mask(c); delete c;
+        return BH_ERR_HIP;
+      }
     }
     // ... and so must the host -> device copy stream be: with every compute queue at high priority,
     // a default-priority queue's packets (the copies' completion markers the staging ring waits on)
@@ -808,7 +820,7 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
       return BH_ERR_HIP;
     }
   }
-  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, acc_lo ? prio_lo : side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, hprio) != hipSuccess) {
     release_mask(c); delete c;

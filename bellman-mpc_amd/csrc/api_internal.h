@@ -63,6 +63,8 @@ struct Domain {
   DevBuf tw_fwd, tw_inv;                  // omega^j, omega^-j, j < m/2
   DevBuf lv_fwd, lv_inv;                  // per-level twiddles, 9 limbs each (launch_level_table)
   DevBuf coset_lo, coset_hi;              // g^i split tables, hi folded with m^-1   (ifft -> coset)
+  DevBuf coset_hi32;                      // the same hi table times 32: the ifft of bls12_381-Montgomery
+                                          // input (R = 2^256) read as device values (R = 2^261)
   DevBuf icoset_lo, icoset_hi;            // g^-i split, hi folded with m^-1        (icoset)
   DevBuf gpow_lo, gpow_hi;                // g^i (no m^-1)                           (coset_fft input)
   DevBuf consts;                          // [0] m^-1, [1] 1/Z(g), [2] one
@@ -344,7 +346,10 @@ bh_status run_h_pipeline(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st
                          uint32_t* hout = nullptr);
 // the same in stages, so that each vector's transforms can be enqueued as its upload lands:
 // run_h_vector(v) for v = 0, 1, 2 in order (v = 2 folds (a*b - c)/Z into a), then run_h_final
-bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v);
+// raw_src: src_abc holds bls12_381 Montgomery words (read in place, the factor 2^5 between the
+// two Montgomery radices folded into the ifft's storing-pass scale); its padding must be zero
+bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, const uint32_t* src_abc, int v,
+                       bool raw_src = false);
 bh_status run_h_final(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, uint32_t* hout);
 bh_status srs_from_bytes(bh_ctx* ctx, int group, const uint8_t* bytes, size_t n, int checked, bool reject_identity,
                          bh_srs* out);

@@ -774,6 +774,18 @@ bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t n
   return full(&params->b_g2, b_aux_used);
 }
 
+// bh_prove's H block reads the uploaded bls12_381-Montgomery a, b, c in place instead of converting
+// them first (BH_H_FUSED_CONVERT=0: the conversion kernel, round 5's first scheme).  Beside the
+// accumulations each extra kernel on the H stream waits for free slots: the round-5 drop-in trace
+// showed a's conversion (a trivial kernel) taking 9.5 ms to get through.
+bool h_fused_convert() {
+  static const bool v = [] {
+    const char* e = getenv("BH_H_FUSED_CONVERT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
 bool prover_serial() {
   static const bool serial = [] {
@@ -1409,6 +1421,25 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if ((s = sort_h_or(sorder[r]))) return s;
   }
   const auto t_sorts = std::chrono::steady_clock::now();
+  // Two accumulation lanes (default; BH_ACC_LANES=1: every accumulation after the first on the main
+  // stream): the accumulations after the first two go to whichever of the two accumulation streams
+  // (the first one's, the main one) has less queued work (mixed additions, a G2 one weighted 2.75x).
+  // Consecutive accumulations on one stream are separated by a barrier (the next kernel dispatches
+  // only once the last block of the previous one is done), and in that moment other streams'
+  // pending kernels take the freed slots (round-5 drop-in trace: 1.4 and 2.9 ms of main-stream idle
+  // before a_aux and h).  Rehearsal N = 8 9.85-9.92 against 10.05-10.23 ms per rank, N = 1 and the
+  // bench within noise (profiles/r05_ab_acc_lanes.txt).
+  static const int acc_lanes = [] {
+    const char* e = getenv("BH_ACC_LANES");
+    return e ? atoi(e) : 2;
+  }();
+  const bool two_lanes = acc_lanes == 2 && first_own && nsmall == 0 && !serial && !ctx->borrowed_streams && nbig > 2;
+  auto acc_cost = [&](int j) {
+    const double e = (double)jobs[j].used * (double)(shapes[j].W ? shapes[j].W : 1);
+    return jobs[j].g2 ? 2.75 * e : e;
+  };
+  double lane_load[2] = {nbig > 0 ? acc_cost(big[0]) : 0.0, 0.0};  // [0] sT, [1] sA
+  for (int q = 1; q < q_first; q++) lane_load[1] += acc_cost(big[q]);
   bool h_done = !h_late;
   for (int q = q_first; q < nbig; q++) {
     if (!h_done && jobs[big[q]].is_h) {
@@ -1416,7 +1447,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       if ((s = sort_h_or(big[q]))) return s;
       h_done = true;
     }
-    if ((s = acc_job(big[q], sA))) return s;
+    hipStream_t sq = sA;
+    if (two_lanes) {
+      const int l = lane_load[0] < lane_load[1] ? 0 : 1;
+      lane_load[l] += acc_cost(big[q]);
+      sq = l == 0 ? sT : sA;
+    }
+    if ((s = acc_job(big[q], sq))) return s;
   }
   if (!h_done && (s = enqueue_h(jev[33]))) return s;  // (no large h job: H still runs)
   if (nbig > 0) last_acc = big[nbig - 1];
@@ -2139,12 +2176,21 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
       uint32_t* abc = ctx->staging.as<uint32_t>();
       BH_TRY_HIP(hipStreamWaitEvent(sH, up.vec[v], 0));
       if (v == 0) BH_TRY_HIP(hipEventRecord(ctx->ev[0], sH));
-      // bls12_381 Montgomery -> device Montgomery into the H block's buffer, zero padding
-      if (nc) launch_fr_convert(w->abc.as<uint32_t>() + (size_t)v * m * 8, abc + (size_t)v * m * 8, nc,
-                                fr_to_dev_const(), 0, sH);
-      if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
-      BH_TRY_HIP(hipGetLastError());
-      bh_status hs = run_h_vector(ctx, D, abc, sH, nullptr, v);
+      bh_status hs;
+      if (h_fused_convert()) {
+        // the ifft's first pass reads the uploaded bls12_381-Montgomery words in place (their
+        // radix folded into its scale, run_h_vector); only the padding is written first
+        uint32_t* raw = const_cast<uint32_t*>(w->abc.as<uint32_t>());
+        if (m > nc) BH_TRY_HIP(hipMemsetAsync(raw + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
+        hs = run_h_vector(ctx, D, abc, sH, raw, v, true);
+      } else {
+        // bls12_381 Montgomery -> device Montgomery into the H block's buffer, zero padding
+        if (nc) launch_fr_convert(w->abc.as<uint32_t>() + (size_t)v * m * 8, abc + (size_t)v * m * 8, nc,
+                                  fr_to_dev_const(), 0, sH);
+        if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
+        BH_TRY_HIP(hipGetLastError());
+        hs = run_h_vector(ctx, D, abc, sH, nullptr, v);
+      }
       if (hs) return hs;
       if (v == 2) {
         // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)
