@@ -281,9 +281,10 @@ class Context:
     def last_stats(self):
         """bh_last_stats: the 10 timing fields, then tables used / large multiexps / table bytes, then
         (after prove() from host buffers) the upload landing times of aux, a, b, c and H's end, ms, then
-        (after an EvaluationDomain transform) its upload / transform / download ms."""
-        out = (ctypes.c_double * 21)()
-        _check(_lib.bh_last_stats(self.h, out, 21))
+        (after an EvaluationDomain transform) its upload / transform / download ms, then the wall time of
+        the G1 and of the G2 accumulations (the union of their launches, which can overlap)."""
+        out = (ctypes.c_double * 23)()
+        _check(_lib.bh_last_stats(self.h, out, 23))
         return list(out)
 
     def scratch_report(self):

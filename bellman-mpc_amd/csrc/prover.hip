@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -1539,6 +1540,31 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ctx->last_timings[9] = (double)g2_adds;
   ctx->last_timings[10] = n_table;
   ctx->last_timings[11] = n_large;
+  // [21] / [22]: wall time during which at least one G1 / G2 accumulation ran (the union of the
+  // launches' event intervals): with two accumulation lanes G1 launches overlap, so the summed
+  // launch time ([2]) counts that time twice
+  ctx->last_timings[21] = ctx->last_timings[22] = 0;
+  if (acc_events_on()) {
+    for (int g = 0; g < 2; g++) {
+      std::vector<std::pair<float, float>> iv;
+      for (int q = 0; q < nbig; q++) {
+        const int j = big[q];
+        if (jobs[j].g2 != (g == 1)) continue;
+        float a = 0, b = 0;
+        if (hipEventElapsedTime(&a, jev[32], jev[2 * j]) == hipSuccess &&
+            hipEventElapsedTime(&b, jev[32], jev[2 * j + 1]) == hipSuccess)
+          iv.push_back({a, b});
+      }
+      std::sort(iv.begin(), iv.end());
+      double tot = 0, cs = -1e30, ce = -1e30;
+      for (const auto& x : iv) {
+        if (x.first > ce) { if (ce > cs) tot += ce - cs; cs = x.first; ce = x.second; }
+        else ce = std::max(ce, (double)x.second);
+      }
+      if (ce > cs) tot += ce - cs;
+      ctx->last_timings[21 + g] = tot;
+    }
+  }
   // bytes of the window tables this proof's multiexps read (each distinct table once): for a
   // shard, its own slices and h share only, not whatever else the Parameters keep resident
   size_t tb = 0;

@@ -321,7 +321,9 @@ bh_status bh_last_timings(const bh_ctx* ctx, double out[10]);
  * read (each distinct table once: for a shard, its own slices); after a bh_prove from host
  * buffers, [13] ms from the call's start until inputs + aux had landed on the device, [14..16]
  * until a, b, c had, [17] until the H block was done; after bh_fft / bh_ifft / bh_coset_fft /
- * bh_icoset_fft, [18] upload, [19] transform, [20] download ms of the last call; n entries are
+ * bh_icoset_fft, [18] upload, [19] transform, [20] download ms of the last call; after a proof,
+ * [21] / [22] the wall time (ms) during which at least one G1 / G2 bucket accumulation ran (the
+ * union of their launches; [2] and [5] sum the launches, which can overlap); n entries are
  * written (missing ones 0). */
 bh_status bh_last_stats(const bh_ctx* ctx, double* out, size_t n);
 
