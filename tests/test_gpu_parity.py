@@ -1055,7 +1055,7 @@ def test_g2_direct_accumulation_equals_default(ctx):
 def test_proof_stats_accumulation_wall_time(ctx):
     """bh_last_stats after a proof with window tables (2^17 constraints): the G1 / G2 launch
     sums [2] / [5], the mixed additions [8] / [9] (one per non-zero digit: at most windows x
-    pairs), and the accumulation wall times [21] / [22] (the union of the launches, which two
+    pairs, with at most 32 windows of c >= 8 bits), and the accumulation wall times [21] / [22] (the union of the launches, which two
     accumulation lanes can overlap): positive, and never more than the launch sums."""
     bh = _bh()
     rounds = (1 << 16) - 1
@@ -1067,4 +1067,4 @@ def test_proof_stats_accumulation_wall_time(ctx):
     assert len(st) == 23
     g1_sum, g2_sum, g1_wall, g2_wall = st[2], st[5], st[21], st[22]
     assert 0 < g1_wall <= g1_sum * 1.0001 and 0 < g2_wall <= g2_sum * 1.0001
-    assert 0 < st[8] <= 16 * st[4] and 0 < st[9] <= 16 * st[7]
+    assert 0 < st[8] <= 32 * st[4] and 0 < st[9] <= 32 * st[7]
