@@ -1003,13 +1003,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     const bh_srs* srs = jobs[j].srs;
     use_table[j] = jobs[j].table_c && srs->win_covers(jobs[j].table_c, jobs[j].blo, jobs[j].bhi);
     if (jobs[j].bk_hi && !use_table[j]) {
-      // a bucket shard without its table (HBM short): rank 0 runs the whole multiexp with plain
-      // windows, the others nothing (the parts still sum to the multiexp)
-      jobs[j].bk_lo = jobs[j].bk_hi = 0;
-      if (shard != 0) {
-        his[j] = los[j];
-        continue;
-      }
+      // a bucket shard without its window table (HBM short when it was to be built): another rank
+      // may well have its table, so a plain-window stand-in here would not sum with the other
+      // ranks' parts -- refuse (bucket shards are opt-in, BH_SHARD_BUCKETS=1)
+      fprintf(stderr, "bellman_hip: bucket shard without its window table (HBM short): set BH_SHARD_BUCKETS=0\n");
+      return BH_ERR_OUT_OF_MEMORY;
     }
     shapes[j] = use_table[j] ? msm_shape_table(his[j] - los[j], srs->win_c)
                              : msm_shape(his[j] - los[j], ctx->window_override);
