@@ -410,7 +410,7 @@ def main():
             "traffic_source": traffic_src,
             "avg_launch_ms": round(acc_ms / launches, 4) if launches else None,
             "avg_launch_source": "HIP events around every launch of the timed steps, on the stream it runs on; "
-                                 "the launches co-run with the G2 accumulation and H as shipped",
+                                 "the launches co-run with the G2 accumulation, with each other (two accumulation lanes) and with H, as shipped",
             "algorithmic_bytes_per_launch": round(alg_per_launch) if launches else None,
             "note": "VALU-bound (XYZZ mixed additions on 29-bit limbs): see DESIGN.md section 4"}
     # the same kernel in the committed profiles of this workload: its rocprofv3 kernel-trace average
