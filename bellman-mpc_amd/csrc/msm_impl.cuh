@@ -323,7 +323,11 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_blocks(const u
   // G2 (448-byte points, one wave per SIMD): the running total `acc` waits in this thread's LDS
   // slot (free until the epilogue) instead of registers, which the compiler otherwise spills
   // to scratch (KB per lane)
+#ifdef BH_G1_REDUCE_LDS
+  constexpr bool acc_lds = true;
+#else
   constexpr bool acc_lds = sizeof(typename C::P) > 256;
+#endif
   typename C::P run = C::identity(), acc = C::identity(), bk = C::identity();
   if (acc_lds) store_point<C>(&lds[i], acc);
   // per bucket k = L-1 .. 0:  bk = partial (+ each continuation partial);  run += bk;  acc += run
