@@ -139,7 +139,7 @@ bh_status enqueue_msm(bh_ctx* ctx, bh_job* job, MsmWorkspace<C>& ws, const bh_sr
     }
   }
   if (!tab) job->sh = msm_shape(n, job->window_override);
-  fit_segments<C>(job->sh, n);
+  fit_segments_E<C>(job->sh, seg_entries(n, set, job->sh.W));
   bh_job_slot* sl = job->slot;
   bool copied = false;
   if (st.key) {  // the same digits already sorted by a recent job: copy its entries

@@ -135,6 +135,13 @@ template <class C>
 void fit_segments(MsmShape& sh, size_t n);
 template <class C>
 void fit_segments_E(MsmShape& sh, size_t E);  // the same for E expected entries
+// The entries fit_segments sizes a multiexp's segments for: n * W for n scalars and W windows
+// (default), or used * W with BH_SEG_USED=1 (`used` = the density set's scalars).  With n * W a
+// half-density multiexp (b_g1_aux, b_g2_aux) gets segments for twice its entries, i.e. half its
+// rounds (1.5 at the 3-round default): alone its last round is half empty (G2 17.2 against 13.4 ms),
+// but in the overlapped proof that is 1.1 ms per 2^22 proof faster than sizing every multiexp for
+// its own entries (profiles/r05_ab_seg_used.txt).
+size_t seg_entries(size_t n, size_t used, int W);
 template <class C>
 hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
                     uint32_t base_offset, const MsmShape& sh);

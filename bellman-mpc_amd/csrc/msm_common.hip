@@ -276,6 +276,15 @@ uint32_t reduce_block_max(bool g2) {
   return g2 ? 128u : 256u;
 }
 
+size_t seg_entries(size_t n, size_t used, int W) {
+  static const bool by_used = [] {
+    const char* e = getenv("BH_SEG_USED");
+    return e && e[0] == '1';
+  }();
+  const size_t k = by_used ? std::min(used, n) : n;
+  return std::max<size_t>(k, 1) * (size_t)std::max(W, 1);
+}
+
 int msm_table_c(size_t n) {
   static const int forced = [] {  // BH_TABLE_C: force the table window size (A/B experiments)
     const char* e = getenv("BH_TABLE_C");

@@ -1028,10 +1028,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       const size_t E = std::max<size_t>((size_t)((double)jobs[j].used * f), 1);
       if (jobs[j].g2) fit_segments_E<G2Ops>(sh, E);
       else fit_segments_E<G1Ops>(sh, E);
-    } else if (jobs[j].g2) {
-      fit_segments<G2Ops>(shapes[j], his[j] - los[j]);
     } else {
-      fit_segments<G1Ops>(shapes[j], his[j] - los[j]);
+      // segments sized for the entries the density set gives (the grid still covers n * W positions)
+      const size_t nj = his[j] - los[j];
+      const size_t used_j = (size_t)((unsigned __int128)jobs[j].used * nj / std::max<size_t>(jobs[j].n, 1));
+      const size_t E = seg_entries(nj, used_j, shapes[j].W);
+      if (jobs[j].g2) fit_segments_E<G2Ops>(shapes[j], E);
+      else fit_segments_E<G1Ops>(shapes[j], E);
     }
     if (jobs[j].table_c) n_large++;
     if (use_table[j]) n_table++;
