@@ -812,11 +812,11 @@ void fit_segments_E(MsmShape& sh, size_t E) {
   // (profiles/r05_ab_acc_rounds.txt): fewer segments are fewer continuation partials and bucket
   // stores, and with the G2 and G1 accumulations sharing the SIMDs a third round balances the
   // finish well enough.  BH_ACC_ROUNDS (BH_ACC_ROUNDS_G1 / BH_ACC_ROUNDS_G2: one group only)
-  static const size_t rounds = [] {
+  static const double rounds = [] {  // (fractional values allowed: A/B)
     const char* e = getenv(std::is_same<C, G1Ops>::value ? "BH_ACC_ROUNDS_G1" : "BH_ACC_ROUNDS_G2");
     if (!e) e = getenv("BH_ACC_ROUNDS");
-    const int r = e ? atoi(e) : 3;
-    return (size_t)(r > 0 ? r : 3);
+    const double r = e ? atof(e) : 3.0;
+    return r > 0.0 ? r : 3.0;
   }();
   // BH_ACC_FILL: fraction of the resident capacity the accumulation occupies per round
   // (the rest stays free for the side streams' short kernels)
@@ -834,7 +834,7 @@ void fit_segments_E(MsmShape& sh, size_t E) {
     const long v = e ? atol(e) : 8;
     return (size_t)(v >= 1 ? v : 8);
   }();
-  const size_t slots = std::max<size_t>((size_t)(rounds * conc * fill) / 256 * 256, 256);
+  const size_t slots = std::max<size_t>((size_t)(rounds * (double)conc * fill) / 256 * 256, 256);
   size_t S = (E + slots - 1) / slots;
   sh.S = (int)std::min<size_t>(std::max<size_t>(S, min_s), (size_t)1 << 16);
 }
