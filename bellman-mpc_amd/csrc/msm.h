@@ -202,9 +202,11 @@ size_t sort_tilecount_words(const MsmShape& sh, size_t n);
 // an already sorted source (src_off: the source's base offset; idx: the target's shard-relative
 // base-index map, -1 = absent).  pos: Emax+1 words scratch; scan_scratch: derive_scratch_words.
 size_t derive_scratch_words(size_t Emax);
+// [b0, b1]: the buckets whose offsets the source sort set (a bucket shard's range; 0, 0: all)
 hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offsets, size_t nbt, size_t Emax, int pre,
                          uint32_t W, uint32_t src_off, const int32_t* idx, uint32_t* pos, uint32_t* scan_scratch,
-                         uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st);
+                         uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st,
+                         size_t b0 = 0, size_t b1 = 0);
 hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_idx, uint32_t base_offset,
                         const MsmShape& sh, uint32_t* tilecounts, uint32_t* tscan_scratch, uint2* recs,
                         uint32_t* entries, uint32_t* counts, uint32_t* offsets, hipStream_t st);

@@ -390,12 +390,14 @@ __global__ void __launch_bounds__(256) k_part_scatter(const uint32_t* scalars, s
 }
 
 // one workgroup per partition; bins = 2^lo_bits <= 4096
+// (partitions p0 .. P-1 of the grid; a bucket shard sorts only its own and passes its end as P,
+// and its last partition also writes offsets[nbt], the shard's entry count)
 __global__ void __launch_bounds__(256) k_part_sort(const uint2* recs, const uint32_t* offs, uint32_t ntiles,
                                                    uint32_t P, int lo_bits, uint32_t nbt, uint32_t* entries,
-                                                   uint32_t* counts, uint32_t* offsets) {
+                                                   uint32_t* counts, uint32_t* offsets, uint32_t p0) {
   __shared__ uint32_t bins[4096];
   __shared__ uint32_t part[256];
-  const uint32_t p = blockIdx.x;
+  const uint32_t p = p0 + blockIdx.x;
   const uint32_t nb = 1u << lo_bits;
   const uint32_t start = offs[(size_t)p * ntiles];
   const uint32_t end = offs[(size_t)(p + 1) * ntiles];  // offs has P*ntiles+1 entries
@@ -426,7 +428,10 @@ __global__ void __launch_bounds__(256) k_part_sort(const uint2* recs, const uint
     bins[b] = run;  // becomes the write cursor
     run += cnt;
   }
-  if (p == P - 1 && threadIdx.x == 0) offsets[nbt] = end;
+  if (p == P - 1 && threadIdx.x == 0) {
+    offsets[nbt] = end;
+    if (((size_t)P << lo_bits) < nbt) offsets[P << lo_bits] = end;  // a shard's end bucket
+  }
   __syncthreads();
   for (uint32_t j = start + threadIdx.x; j < end; j += 256) {
     const uint2 r = recs[j];
@@ -469,20 +474,26 @@ __global__ void __launch_bounds__(256) k_derive_write(const uint32_t* src_entrie
   if (derive_keep(src_entries[j], pre, W, src_off, idx, &ne)) dst_entries[pos[j]] = ne;
 }
 
-__global__ void __launch_bounds__(256) k_derive_offsets(const uint32_t* src_offsets, size_t nbt, const uint32_t* pos,
-                                                        uint32_t* dst_offsets, uint32_t* dst_counts) {
-  const size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nbt) return;
+// buckets [b0, b1] (b1 <= nbt; a bucket shard's range, whose offsets alone are set), and
+// dst_offsets[nbt] = the derived entry count
+__global__ void __launch_bounds__(256) k_derive_offsets(const uint32_t* src_offsets, size_t nbt, size_t b0, size_t b1,
+                                                        const uint32_t* pos, uint32_t* dst_offsets,
+                                                        uint32_t* dst_counts) {
+  const size_t b = b0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > b1) return;
   const uint32_t o = pos[src_offsets[b]];
   dst_offsets[b] = o;
-  if (b < nbt) dst_counts[b] = pos[src_offsets[b + 1]] - o;
+  if (b < b1) dst_counts[b] = pos[src_offsets[b + 1]] - o;
+  if (b == b1 && b1 < nbt) dst_offsets[nbt] = o;
 }
 
 size_t derive_scratch_words(size_t Emax) { return scan_scratch_words(Emax + 1) + 64; }
 
 hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offsets, size_t nbt, size_t Emax, int pre,
                          uint32_t W, uint32_t src_off, const int32_t* idx, uint32_t* pos, uint32_t* scan_scratch,
-                         uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st) {
+                         uint32_t* dst_entries, uint32_t* dst_counts, uint32_t* dst_offsets, hipStream_t st,
+                         size_t b0, size_t b1) {
+  if (b1 == 0 || b1 > nbt) b1 = nbt;
   const uint32_t* src_E = src_offsets + nbt;
   hipLaunchKernelGGL(k_derive_mark, dim3(blocks_for(Emax + 1, 256)), dim3(256), 0, st, src_entries, src_E, Emax, pre, W,
                      src_off, idx, pos);
@@ -490,8 +501,8 @@ hipError_t derive_sorted(const uint32_t* src_entries, const uint32_t* src_offset
   exclusive_scan_b(pos, pos, Emax + 1, scan_scratch, st, src_E);
   hipLaunchKernelGGL(k_derive_write, dim3(blocks_for(Emax, 256)), dim3(256), 0, st, src_entries, src_E, pre, W, src_off,
                      idx, pos, dst_entries);
-  hipLaunchKernelGGL(k_derive_offsets, dim3(blocks_for(nbt + 1, 256)), dim3(256), 0, st, src_offsets, nbt, pos,
-                     dst_offsets, dst_counts);
+  hipLaunchKernelGGL(k_derive_offsets, dim3(blocks_for(b1 - b0 + 1, 256)), dim3(256), 0, st, src_offsets, nbt, b0, b1,
+                     pos, dst_offsets, dst_counts);
   return hipGetLastError();
 }
 
@@ -533,11 +544,17 @@ hipError_t sort_entries(const uint32_t* d_scalars, size_t n, const int32_t* d_id
   const uint32_t phi = sh.bucket_shard() ? sh.bk_hi >> lo : P;
   hipLaunchKernelGGL(k_part_count, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, cfg, lo, P, nt, plo, phi,
                      tilecounts);
-  exclusive_scan(tilecounts, tilecounts, tw, tscan_scratch, st);
+  // a shard scans only its partitions' slice of the partition-major tile counts (the word after
+  // the slice is the next partition's first count, 0, or the extra last word): 1/N of the scan
+  if (sh.bucket_shard())
+    exclusive_scan(tilecounts + (size_t)plo * nt, tilecounts + (size_t)plo * nt, (size_t)(phi - plo) * nt + 1,
+                   tscan_scratch, st);
+  else
+    exclusive_scan(tilecounts, tilecounts, tw, tscan_scratch, st);
   hipLaunchKernelGGL(k_part_scatter, dim3(nt), dim3(256), P * 4, st, d_scalars, n, d_idx, base_offset, cfg, lo, P,
                      nt, plo, phi, tilecounts, recs);
-  hipLaunchKernelGGL(k_part_sort, dim3(P), dim3(256), 0, st, recs, tilecounts, nt, P, lo, (uint32_t)nbt, entries,
-                     counts, offsets);
+  hipLaunchKernelGGL(k_part_sort, dim3(phi - plo), dim3(256), 0, st, recs, tilecounts, nt, phi, lo, (uint32_t)nbt,
+                     entries, counts, offsets, plo);
   return hipGetLastError();
 }
 

@@ -682,7 +682,8 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   uint32_t e_cur = entry(start);
   issue(e_cur);
   uint32_t e_next = (start + 1 < end) ? entry(start + 1) : 0u;
-  uint32_t b = find_bucket(offsets, nbt, start);
+  // (searched within [b_lo, b_hi]: a bucket shard's sort leaves the other buckets' offsets unset)
+  uint32_t b = b_lo + find_bucket(offsets + b_lo, b_hi - b_lo, start);
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
   if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
@@ -764,7 +765,7 @@ k_accumulate_g2d(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
   auto entry = [&](uint32_t j) { return entries ? entries[j] : j; };
   const uint32_t e_cur = entry(start);
   const uint32_t e_next = (start + 1 < end) ? entry(start + 1) : 0u;
-  const uint32_t b = find_bucket(offsets, nbt, start);
+  const uint32_t b = b_lo + find_bucket(offsets + b_lo, b_hi - b_lo, start);
   const uint32_t next = offsets[b + 1];
   const bool started_here = offsets[b] >= pos0;
   if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
@@ -980,10 +981,15 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
   if (n > 0) {
     const size_t Emax = n * (size_t)sh.W;
     const size_t segs = (Emax + sh.S - 1) / sh.S;
+    uint32_t launch_range_first = 0, launch_range_end = 0;
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
     const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
+    if (sh.bucket_shard()) {  // only the shard's buckets are sorted (their offsets alone are set)
+      launch_range_first = sh.bk_lo;
+      launch_range_end = sh.bk_hi;
+    }
     auto launch = [&](uint32_t lo, uint32_t hi) {
       if constexpr (!std::is_same<C, G1Ops>::value) {
         if (g2_direct()) {
@@ -997,7 +1003,8 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
                          ws.offsets, (uint32_t)nbt, d_bases, rec, (uint32_t)sh.S, lo, hi, ws.bucket_sums, ws.conts,
                          ws.cont_bucket);
     };
-    launch(0u, cut);
+    if (sh.bucket_shard()) launch(launch_range_first, launch_range_end);
+    else launch(0u, cut);
     if (sh.halves) {
       if (timing && timing->ev_half) hipEventRecord(timing->ev_half, st);
       launch(cut, (uint32_t)nbt);
@@ -1098,7 +1105,7 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
   SpanSrc dev;
   if (max_span < 0 && d_span_words) {  // device-decided: fold up to REDUCE_FOLD_SPAN, else k_cont_seq
     dev.words = d_span_words;
-    dev.g = max_span_blocks((size_t)sh.Wb * sh.NB);
+    dev.g = max_span_blocks((size_t)sh.Wb * sh.red_nb());  // (sort_job's k_max_span range)
     dev.fold_span = (uint32_t)REDUCE_FOLD_SPAN;
     dev.seq_max = (uint32_t)cont_seq_max();
   }

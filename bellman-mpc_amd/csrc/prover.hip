@@ -1136,7 +1136,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       BH_TRY_HIP(ctx->dscan2.alloc(derive_scratch_words(Emax) * 4));
       BH_TRY_HIP(hipStreamWaitEvent(st, jev[16 + dsrc], 0));
       BH_TRY_HIP(derive_sorted(se, so, nbt, Emax, sh.pre, (uint32_t)sh.W, (uint32_t)los[dsrc], ix, pos,
-                               ctx->dscan2.as<uint32_t>(), de, dc, dof, st));
+                               ctx->dscan2.as<uint32_t>(), de, dc, dof, st, sh.bucket_shard() ? sh.bk_lo : 0u,
+                               sh.bucket_shard() ? sh.bk_hi : 0u));
       sorted_from[j] = j;  // a sort of its own from here on (copies may take it)
     } else if (src >= 0) {
       const MsmShape& sh = shapes[j];
@@ -1165,9 +1166,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     // continuation-tree depth of this multiexp (read by its tail, so it launches only the
     // levels that can do work)
     const MsmShape& shj = shapes[j];
-    const uint32_t* cnt = J.g2 ? ctx->pw2[J.out].counts : ctx->pw1[J.out].counts;
-    const uint32_t* off = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
-    BH_TRY_HIP(max_span(cnt, off, (size_t)shj.Wb * shj.NB, (uint32_t)shj.S,
+    // (a bucket shard: over its own buckets, the only ones its sort set)
+    const uint32_t* cnt = (J.g2 ? ctx->pw2[J.out].counts : ctx->pw1[J.out].counts) + shj.red_lo();
+    const uint32_t* off = (J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets) + shj.red_lo();
+    BH_TRY_HIP(max_span(cnt, off, (size_t)shj.Wb * shj.red_nb(), (uint32_t)shj.S,
                         ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS, ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS,
                         st));
     BH_TRY_HIP(hipEventRecord(jev[16 + j], st));
@@ -1219,7 +1221,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (n >= SMALL_JOB) {
       if (host_span) {
         BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
-        span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS, (size_t)shapes[j].Wb * shapes[j].NB);
+        span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS,
+                                  (size_t)shapes[j].Wb * shapes[j].red_nb());
       } else {
         dspan = ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS;
       }
