@@ -1477,6 +1477,17 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (t_lane.after_accs) t_lane.after_accs();
   if (t_lane.before_tails) t_lane.before_tails();
   if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = sT;
+  // BH_G2_TAIL_FULL=1 (A/B): the G2 multiexps' reduction tails on the witness-copy stream (every CU,
+  // high priority; a resident proof never copies on it, bh_prove's uploads are done long before)
+  // instead of a quarter-CU tail stream: at N = 8 the G2 tail (continuation fold 3.7 ms, reduction
+  // 2.3 ms on 64 CUs) ends the rank's proof (gpurun_out/r5rt trace)
+  static const bool g2_tail_full = [] {
+    const char* e = getenv("BH_G2_TAIL_FULL");
+    return e && e[0] == '1';
+  }();
+  if (g2_tail_full && !serial && !ctx->borrowed_streams)
+    for (int q = 0; q + 1 < nbig; q++)
+      if (jobs[big[q]].g2) tails[q] = ctx->h2d;
   for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
     BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
