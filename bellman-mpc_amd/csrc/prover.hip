@@ -799,13 +799,16 @@ bool prover_serial() {
 // resident threads of the G1 bucket reduction (k_reduce_blocks) on every CU (full) or on the
 // CU-masked tail streams' quarter of them
 size_t reduce_resident_threads(bh_ctx* ctx, bool full) {
-  static size_t per_cu = 0;
-  static int ncu = 0;
-  if (!per_cu) {
-    per_cu = reduce_blocks_resident_per_cu_g1();
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-  }
-  const int cus = full ? ncu : std::max(1, ncu / 4);
+  // occupancy is a property of the kernel (one code object for every device); the CU count is
+  // the context's device's, read once per device (contexts on several devices, concurrently)
+  static const size_t per_cu = reduce_blocks_resident_per_cu_g1();
+  static std::once_flag once[64];
+  static int ncu[64];
+  const int d = ctx->device & 63;
+  std::call_once(once[d], [&] {
+    if (hipDeviceGetAttribute(&ncu[d], hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess) ncu[d] = 1;
+  });
+  const int cus = full ? ncu[d] : std::max(1, ncu[d] / 4);
   return per_cu * (size_t)std::max(cus, 1);
 }
 
@@ -1235,8 +1238,13 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
                                  dspan));
     return BH_OK;
   };
-  BH_TRY_HIP(hipEventRecord(jev[33], sS));
-  BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
+  // the H stream follows the density maps and sorts enqueued so far -- unless the uploading
+  // thread is enqueueing H on it vector by vector (bh_prove): those kernels are ordered behind
+  // their uploads already, and a wait issued here would land between them at a random point
+  if (!(up && up->on_vector)) {
+    BH_TRY_HIP(hipEventRecord(jev[33], sS));
+    BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
+  }
   int big[8], nbig = 0, small[8], nsmall = 0;
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];
@@ -2253,8 +2261,12 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
   st = compute_msms_sync(ctx, params, w, 0, 1, r1, r2, nullptr, true, &up);
   uploader.join();
   (void)hipStreamSynchronize(ctx->h2d);
-  if (st) return st;
-  if (ust) return ust;
+  if (st || ust) {
+    // compute_msms' drain may have run before the uploader finished enqueueing H on the H
+    // stream (staging, hbuf): drain every stream once more so no later call races those kernels
+    ctx_sync_all(ctx);
+    return st ? st : ust;
+  }
   // upload landing times from the call's start (bh_last_stats [13..16): aux, a, b, c) and, from
   // compute_msms, the H block's end ([12] stays the table bytes)
   {

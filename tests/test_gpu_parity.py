@@ -331,6 +331,17 @@ def test_window_tables_match_plain_windows(ctx, logc):
     assert bh.prove_witness(ctx, params, w, 27134, 17146) == plain
     parts = b"".join(bh.prove_witness_partial(ctx, params, w, k, 2) for k in range(2))
     assert bh.proof_from_partials(params.vk_bytes(), parts, 2, 27134, 17146) == plain
+    if logc == 22:
+        # the benchmark's own proof (C3) equals the oracle port's proof of the same CRS and
+        # witness, recorded in tests/golden/port_proofs.json by tools/cpu_baseline_full.py
+        # --fixture (prover.rs:315-349 output)
+        fx = _port_proof(22)
+        assert hashlib.sha256(params.write()).hexdigest() == fx["params_sha256"]
+        assert plain.hex() == fx["proof_port"]
+        # the drop-in entry point at the headline size: bh_prove from host buffers (the
+        # ProvingAssignment in bls12_381's layouts) gives the same bytes
+        asg = bh.chain_assignment(rounds)
+        assert bh.prove(ctx, params, asg, 27134, 17146).hex() == fx["proof_port"]
 
 
 def test_checked_load_rejects_points_outside_subgroup(ctx):
