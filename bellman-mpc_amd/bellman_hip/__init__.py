@@ -28,6 +28,7 @@ _MONT_R = pow(2, 256, R_MODULUS)
 _MONT_RINV = pow(_MONT_R, -1, R_MODULUS)
 
 BH_OK = 0
+BH_ERR_INVALID_ARGUMENT = 10
 BH_G1, BH_G2 = 1, 2
 BH_SCALARS_CANONICAL, BH_SCALARS_MONTGOMERY = 0, 1
 
@@ -140,6 +141,21 @@ def _load():
         "bh_scalars_sync": (I, [P]),
         "bh_scalars_stamps": (I, [P, P]),
         "bh_scratch_report": (I, [P, P, S, ctypes.c_char_p, S]),
+        "bh_evdom_from_coeffs": (I, [P, P, S, P]),
+        "bh_evdom_size": (I, [P, P, P]),
+        "bh_evdom_fft": (I, [P]),
+        "bh_evdom_ifft": (I, [P]),
+        "bh_evdom_coset_fft": (I, [P]),
+        "bh_evdom_icoset_fft": (I, [P]),
+        "bh_evdom_distribute_powers": (I, [P, P]),
+        "bh_evdom_divide_by_z_on_coset": (I, [P]),
+        "bh_evdom_mul_assign": (I, [P, P]),
+        "bh_evdom_sub_assign": (I, [P, P]),
+        "bh_evdom_read": (I, [P, P, S]),
+        "bh_evdom_write": (I, [P, P, S]),
+        "bh_evdom_into_scalars": (I, [P, S, P]),
+        "bh_evdom_sync": (I, [P]),
+        "bh_evdom_free": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -166,6 +182,10 @@ EXPORTED_SYMBOLS = [
     "bh_multiexp_submit", "bh_multiexp_wait", "bh_prove_batch", "bh_verify_proof", "bh_verify_batch",
     "bh_params_vector", "bh_scalars_upload", "bh_compute_h_scalars", "bh_scalars_len", "bh_scalars_free",
     "bh_multiexp_submit_scalars", "bh_scalars_sync", "bh_scratch_report", "bh_scalars_stamps",
+    "bh_evdom_from_coeffs", "bh_evdom_size", "bh_evdom_fft", "bh_evdom_ifft", "bh_evdom_coset_fft",
+    "bh_evdom_icoset_fft", "bh_evdom_distribute_powers", "bh_evdom_divide_by_z_on_coset", "bh_evdom_mul_assign",
+    "bh_evdom_sub_assign", "bh_evdom_read", "bh_evdom_write", "bh_evdom_into_scalars", "bh_evdom_sync",
+    "bh_evdom_free",
 ]
 BH_VEC_H, BH_VEC_L, BH_VEC_A, BH_VEC_B_G1, BH_VEC_B_G2 = range(5)
 PARTIAL_BYTES = 960
@@ -540,6 +560,121 @@ class EvaluationDomain:
         return fr_from_mont(self.coeffs)
 
 
+class ResidentEvaluationDomain:
+    """EvaluationDomain (domain.rs:21-190) whose coefficients stay in HBM between calls
+    (bh_evdom_*): the methods enqueue device work, only as_ref / into_coeffs / into_scalars read
+    back.  from_coeffs reads the host array asynchronously (kept referenced until sync)."""
+
+    def __init__(self, ctx, coeffs):
+        arr = coeffs if isinstance(coeffs, np.ndarray) else fr_to_mont(coeffs)
+        arr = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 4)
+        h = ctypes.c_void_p()
+        _check(_lib.bh_evdom_from_coeffs(ctx.h, _ptr(arr) if arr.shape[0] else None, arr.shape[0], ctypes.byref(h)),
+               "from_coeffs")
+        self.ctx, self.h, self._keep = ctx, h, arr
+        m = ctypes.c_size_t()
+        e = ctypes.c_uint32()
+        _check(_lib.bh_evdom_size(h, ctypes.byref(m), ctypes.byref(e)))
+        self.m, self.exp = m.value, e.value
+
+    from_coeffs = classmethod(lambda cls, ctx, coeffs: cls(ctx, coeffs))
+
+    def _run(self, f, *args):
+        _check(f(self.h, *args))
+
+    def fft(self):
+        self._run(_lib.bh_evdom_fft)
+
+    def ifft(self):
+        self._run(_lib.bh_evdom_ifft)
+
+    def coset_fft(self):
+        self._run(_lib.bh_evdom_coset_fft)
+
+    def icoset_fft(self):
+        self._run(_lib.bh_evdom_icoset_fft)
+
+    def divide_by_z_on_coset(self):
+        self._run(_lib.bh_evdom_divide_by_z_on_coset)
+
+    def distribute_powers(self, g):
+        gm = fr_to_mont([g])[0]
+        self._run(_lib.bh_evdom_distribute_powers, _ptr(gm))
+
+    def mul_assign(self, other):
+        self._run(_lib.bh_evdom_mul_assign, other.h)
+
+    def sub_assign(self, other):
+        self._run(_lib.bh_evdom_sub_assign, other.h)
+
+    def sync(self):
+        """bh_evdom_sync: the upload has read the host array."""
+        self._run(_lib.bh_evdom_sync)
+        self._keep = None
+
+    def as_mont(self, n=None):
+        """as_ref (domain.rs:28-32): the first n (default m) coefficients, (n,4) Montgomery."""
+        n = self.m if n is None else n
+        out = np.zeros((max(n, 1), 4), dtype=np.uint64)
+        self._run(_lib.bh_evdom_read, _ptr(out), n)
+        return out[:n]
+
+    def as_ref(self):
+        return fr_from_mont(self.as_mont())
+
+    def into_coeffs(self):
+        return self.as_ref()
+
+    def write(self, coeffs):
+        """as_mut written back (domain.rs:34-38): replaces the coefficients (zero padded)."""
+        arr = coeffs if isinstance(coeffs, np.ndarray) else fr_to_mont(coeffs)
+        arr = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 4)
+        self._run(_lib.bh_evdom_write, _ptr(arr) if arr.shape[0] else None, arr.shape[0])
+        self._keep = arr
+
+    def into_scalars(self, n):
+        """prover.rs:226-231 on the device: the first n coefficients as a Scalars vector
+        (canonical), ready for multiexp_async; consumes the domain."""
+        h = ctypes.c_void_p()
+        self._run(_lib.bh_evdom_into_scalars, n, ctypes.byref(h))
+        return Scalars(self.ctx, _handle=h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.bh_evdom_free(self.h)
+            self.h = None
+        self._keep = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def compute_h_resident(ctx, a, b, c, scalars=False):
+    """The H block through the resident EvaluationDomain exactly as create_proof drives it
+    (prover.rs:210-231, ten calls): h as a list of m-1 ints, or as a device Scalars."""
+    da, db, dc = (ResidentEvaluationDomain(ctx, x) for x in (a, b, c))
+    try:
+        da.ifft()
+        da.coset_fft()
+        db.ifft()
+        db.coset_fft()
+        dc.ifft()
+        dc.coset_fft()
+        da.mul_assign(db)
+        da.sub_assign(dc)
+        da.divide_by_z_on_coset()
+        da.icoset_fft()
+        if scalars:
+            return da.into_scalars(da.m - 1)
+        return fr_from_mont(da.as_mont(da.m - 1))
+    finally:
+        for d in (da, db, dc):
+            d.close()
+
+
 def compute_h(ctx, a, b, c):
     """H block of create_proof (prover.rs:210-231) -> list of m-1 ints."""
     A, B, C = (x if isinstance(x, np.ndarray) else fr_to_mont(x) for x in (a, b, c))
@@ -805,15 +940,20 @@ def prove(ctx, params, asg, r, s):
     return out.tobytes()
 
 
-def prove_seam(ctx, params, asg, r, s, profile=None):
+def prove_seam(ctx, params, asg, r, s, profile=None, h_via_domain=False):
     """create_proof after synthesis (prover.rs:206-349) through the multiexp seam alone, as a
     Rust caller that swaps only multiexp() and the H block sees it: h on the device
     (bh_compute_h_scalars), the assignments uploaded once (the Arcs of prover.rs:233-250), the
     eight multiexps in flight on the Parameters' own vectors (get_h ... get_b_g2, so their window
     tables apply), waited, and the proof assembled on the host (prover.rs:315-349).
-    asg: dict as returned by chain_assignment.  Byte-equal to prove()."""
+    asg: dict as returned by chain_assignment.  Byte-equal to prove().  h_via_domain: the H block
+    through the resident EvaluationDomain's ten calls instead (compute_h_resident), h handed to
+    the multiexp as a device vector (into_scalars), as a caller swapping EvaluationDomain too."""
     ni, na = asg["inputs"].shape[0], asg["aux"].shape[0]
-    h = compute_h_scalars(ctx, asg["a"], asg["b"], asg["c"])
+    if h_via_domain:
+        h = compute_h_resident(ctx, asg["a"], asg["b"], asg["c"], scalars=True)
+    else:
+        h = compute_h_scalars(ctx, asg["a"], asg["b"], asg["c"])
     inp = Scalars(ctx, asg["inputs"], montgomery=True)
     aux = Scalars(ctx, asg["aux"], montgomery=True)
     a_aux = DensityWords(asg["a_aux_density"], na)
@@ -826,7 +966,7 @@ def prove_seam(ctx, params, asg, r, s, profile=None):
                multiexp_async(ctx, B1, 0, b_in, inp), multiexp_async(ctx, B1, b_in_total, b_aux, aux),
                multiexp_async(ctx, B2, 0, b_in, inp), multiexp_async(ctx, B2, b_in_total, b_aux, aux)]
     partial = b"".join(w.wait() for w in waiters)
-    if profile is not None:  # the h producer's stage times of this call (bh_scalars_stamps)
+    if profile is not None and not h_via_domain:  # the h producer's stage times (bh_scalars_stamps)
         profile.append(h.stamps())
     return proof_from_partials(params.vk_bytes(), partial, 1, r, s)
 

@@ -483,7 +483,7 @@ bh_status multiexp_check(const bh_srs* bases, size_t base_offset, const uint64_t
 static Fr fr_small(uint64_t v) { uint64_t x[4] = {v, 0, 0, 0}; return from_int<4>(x); }
 static Fr fr_pow_u64(const Fr& a, uint64_t e) { return pow_vartime(a, &e, 1); }
 
-static bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, const Fr& hi_scale, int L,
+bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, const Fr& hi_scale, int L,
                                     int lo_bits) {
   const size_t nlo = (size_t)1 << lo_bits;
   const size_t nhi = (size_t)1 << (L > lo_bits ? L - lo_bits : 0);
@@ -926,6 +926,14 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   for (bh_ctx* v : ctx->lanes) bh_ctx_destroy(v);
   ctx->lanes.clear();
   (void)hipSetDevice(ctx->device);
+  {  // the EvaluationDomain uploader: finish the queued copies, then stop
+    {
+      std::lock_guard<std::mutex> lk(ctx->dup.mu);
+      ctx->dup.stop = true;
+    }
+    ctx->dup.cv.notify_all();
+    if (ctx->dup.th.joinable()) ctx->dup.th.join();
+  }
   {  // bh_compute_h_scalars producers still uploading: their deferred multiexps enqueue first
     std::unique_lock<std::mutex> lk(ctx->bg.count_mu);
     ctx->bg.cv.wait(lk, [&] { return ctx->bg.active == 0; });
@@ -951,6 +959,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
   for (auto& w : ctx->pw1) w.release();
   for (auto& w : ctx->pw2) w.release();
   ctx->domains.clear();
+  ctx->evdom_pool.clear();
   for (auto& e : ctx->ev) if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->jev) if (e) (void)hipEventDestroy(e);
   if (ctx->host_out1) (void)hipHostFree(ctx->host_out1);
@@ -1235,7 +1244,7 @@ void scalar_pool_drain(int device) {
   pl.held = 0;
 }
 
-static bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out) {
+bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out) {
   static std::atomic<uint64_t> next_id{1};
   auto buf = std::make_shared<bh_scalar_buf>();
   buf->device = ctx->device;
@@ -1285,6 +1294,42 @@ bh_status bh_scalars_free(bh_scalars* s) {
   return BH_OK;
 }
 
+}  // extern "C"
+
+namespace bh {
+// the background copy machinery (caller holds ctx->bg.mu): streams, pinned ring, memcpy workers
+bh_status bg_init(bh_ctx* ctx) {
+  auto& bg = ctx->bg;
+  if (bg.st) return BH_OK;
+  // high priority, like the prover's H stream: its passes must not starve beside the
+  // accumulations (the multiexp on h sorts only after them)
+  int lo = 0, hi = 0;
+  BH_TRY_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  BH_TRY_HIP(hipStreamCreateWithPriority(&bg.st, hipStreamNonBlocking, hi));
+  BH_TRY_HIP(hipStreamCreateWithPriority(&bg.cst, hipStreamNonBlocking, hi));  // (as ctx->h2d)
+  for (auto& e : bg.vec) BH_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  BH_TRY_HIP(bg.ring.init());
+  bg.pool.reset(new HostPool(3));
+  return BH_OK;
+}
+
+// dst (device) <- src (pageable host) on bg.cst, in 16 MB pieces (one ring slot), paused while a
+// bh_scalars_upload streams (the assignments feed the first sorts; H is needed last).  Returns
+// once the host buffer has been read.
+bh_status bg_copy(bh_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  auto& bg = ctx->bg;
+  const size_t piece = (size_t)16 << 20;
+  for (size_t off = 0; off < bytes; off += piece) {
+    while (bg.fg_uploads.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    BH_TRY_HIP(bg.ring.copy(*bg.pool, reinterpret_cast<uint8_t*>(dst) + off,
+                            reinterpret_cast<const uint8_t*>(src) + off, std::min(piece, bytes - off), bg.cst));
+  }
+  return BH_OK;
+}
+}  // namespace bh
+
+extern "C" {
+
 bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c, size_t nc,
                                bh_scalars** h_out) {
   if (!ctx || (nc && (!a || !b || !c)) || !h_out) return BH_ERR_INVALID_ARGUMENT;
@@ -1317,17 +1362,8 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
       auto& bg = ctx->bg;
       std::lock_guard<std::mutex> lk(bg.mu);
       BH_TRY_HIP(hipSetDevice(ctx->device));
-      if (!bg.st) {
-        // high priority, like the prover's H stream: its passes must not starve beside the
-        // accumulations (the multiexp on h sorts only after them)
-        int lo = 0, hi = 0;
-        BH_TRY_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        BH_TRY_HIP(hipStreamCreateWithPriority(&bg.st, hipStreamNonBlocking, hi));
-        BH_TRY_HIP(hipStreamCreateWithPriority(&bg.cst, hipStreamNonBlocking, hi));  // (as ctx->h2d)
-        for (auto& e : bg.vec) BH_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        BH_TRY_HIP(bg.ring.init());
-        bg.pool.reset(new HostPool(3));
-      }
+      bh_status bs = bg_init(ctx);
+      if (bs) return bs;
       // a|b|c: the copies (bg.cst) start after the previous producer's H (bg.st) is done with it;
       // each vector's transforms (bg.st) start as soon as its own copy has landed
       BH_TRY_HIP(bg.abc.alloc(3 * m * 32));
@@ -1347,15 +1383,7 @@ bh_status bh_compute_h_scalars(bh_ctx* ctx, const uint64_t* a, const uint64_t* b
         uint32_t* dst = abc + (size_t)v * m * 8;
         if (m > nc) BH_TRY_HIP(hipMemsetAsync(dst + nc * 8, 0, (m - nc) * 32, bg.cst));
         if (nc) {
-          // in 16 MB pieces, paused while a bh_scalars_upload streams (the assignments feed the
-          // first sorts; H is needed last)
-          const size_t piece = (size_t)16 << 20;  // one ring slot
-          for (size_t off = 0; off < nc * 32; off += piece) {
-            while (bg.fg_uploads.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
-            BH_TRY_HIP(bg.ring.copy(*bg.pool, reinterpret_cast<uint8_t*>(dst) + off,
-                                    reinterpret_cast<const uint8_t*>(src[v]) + off, std::min(piece, nc * 32 - off),
-                                    bg.cst));
-          }
+          if ((bs = bg_copy(ctx, dst, src[v], nc * 32))) return bs;
           stamp("uploaded", v);
         }
         raw->stamps[v] = since();

@@ -5,6 +5,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -70,6 +71,21 @@ struct Domain {
   DevBuf consts;                          // [0] m^-1, [1] 1/Z(g), [2] one
   int lo_bits = 0;
   Fr minv, zinv;
+};
+
+// a device-resident EvaluationDomain's buffers (evaldomain.hip): coefficients, permute scratch,
+// post-scale table, and the event after the last work that read them on ctx->stream; a freed
+// domain's set is pooled by its context for the next one (no hipFree / hipMalloc per call)
+struct EvdomBufs {
+  DevBuf buf, tmp, post;
+  hipEvent_t idle = nullptr, landed = nullptr;  // landed: the last upload into buf (bg.cst)
+  EvdomBufs() = default;
+  EvdomBufs(const EvdomBufs&) = delete;
+  EvdomBufs& operator=(const EvdomBufs&) = delete;
+  ~EvdomBufs() {
+    if (idle) (void)hipEventDestroy(idle);
+    if (landed) (void)hipEventDestroy(landed);
+  }
 };
 
 struct bh_ctx_impl;
@@ -164,6 +180,9 @@ constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use pla
 // another proof's multiexps run (a seam caller's Arcs) would hold every HIP call of the process
 // behind them.  take: a buffer of at least `bytes` or null; give: keeps it (bounded) or frees it.
 extern "C" void* scalar_pool_take(int device, size_t bytes, size_t* got);
+struct bh_scalar_buf;
+// a device scalar vector of n canonical scalars (pooled), its ready event created
+extern "C" bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out);
 extern "C" void scalar_pool_give(int device, void* p, size_t bytes);
 extern "C" void scalar_pool_drain(int device);  // frees every pooled buffer of the device
 
@@ -302,6 +321,17 @@ struct bh_ctx {
     std::condition_variable cv;
     int active = 0;
   } bg;
+  // device-resident EvaluationDomains (evaldomain.hip): one thread uploads their coefficients in
+  // call order through the bg copy machinery (under bg.mu), so an ifft can run while the next
+  // domain is still streaming in; bh_ctx_destroy drains and joins it
+  struct DomainUploads {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    std::thread th;
+    bool stop = false;
+  } dup;
+  std::vector<std::unique_ptr<bh::EvdomBufs>> evdom_pool;  // freed domains' buffers (under mu)
   // bh_multiexp_submit / _wait (jobs.hip): recycled per-job resources under their own lock (a
   // submit never waits behind a proof holding mu)
   std::shared_ptr<bh_job_registry> jobs = std::make_shared<bh_job_registry>();
@@ -318,6 +348,14 @@ extern "C" bh_status ctx_create_lane(bh_ctx* primary, bh_ctx** out);  // (define
 
 namespace bh {
 bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out);
+// background copies (caller holds ctx->bg.mu): create the bg streams / ring once; copy pageable
+// host bytes to the device on bg.cst (returns once the host buffer has been read)
+bh_status bg_init(bh_ctx* ctx);
+// split power tables g^i = lo[i & mask] * hi[i >> lo_bits] (hi scaled by hi_scale), uploaded on
+// ctx->stream and synchronised (caller holds ctx->mu)
+bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, const Fr& hi_scale, int L,
+                             int lo_bits);
+bh_status bg_copy(bh_ctx* ctx, void* dst, const void* src, size_t bytes);
 // wait for every stream of the context (error paths, teardown)
 void ctx_sync_all(bh_ctx* ctx);
 // host <-> device Fr helpers

@@ -40,8 +40,14 @@ void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t
 void launch_level_table(uint32_t* lv, int L, const uint32_t* tw, hipStream_t st);
 void launch_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo, const uint32_t* hi, int lo_bits,
                     hipStream_t st);
+// a[i] *= lo[i & mask] * hi[i >> lo_bits] (or the constant c when hi is null); rev_L >= 0: a is
+// in bit-reversed order (2^rev_L elements) and position i takes the factor of index brev(i)
 void launch_scale(uint32_t* a, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits, const uint32_t* c,
-                  hipStream_t st);
+                  hipStream_t st, int rev_L = -1);
+// out[j] = in[j] * k for unpacked (9-limb) table entries, reduced below r
+void launch_table_scale(uint32_t* out, const uint32_t* in, size_t n, const FrConst& k, hipStream_t st);
+// a = a * k - b (packed)
+void launch_scale_sub(uint32_t* a, const uint32_t* b, size_t n, const FrConst& k, hipStream_t st);
 // op 0: a *= b ; 1: a -= b ; 2: a = (a*b - c) * k
 void launch_pointwise(uint32_t* a, const uint32_t* b, const uint32_t* c, size_t n, int op, const uint32_t* k,
                       hipStream_t st);

@@ -300,14 +300,39 @@ __global__ void __launch_bounds__(256) k_permute(const uint32_t* in, uint32_t* o
   st_packed(out, brev(i, L), x);
 }
 
-// a[i] *= factor(i)  or a[i] *= c (constant, unpacked) when lo == nullptr
+// a[i] *= factor(i)  or a[i] *= c (constant, unpacked) when hi == nullptr.  rev_L >= 0: a holds
+// 2^rev_L elements in bit-reversed order, so the factor of position i is factor(brev(i))
 __global__ void __launch_bounds__(256) k_scale(uint32_t* a, uint32_t n, const uint32_t* lo, const uint32_t* hi,
-                                               int lo_bits, const uint32_t* c) {
+                                               int lo_bits, const uint32_t* c, int rev_L) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DFr x = ld_packed(a, i);
-  const DFr f = hi ? pow_factor(lo, hi, lo_bits, i) : ld_limbs(c, 0);
+  const DFr f = hi ? pow_factor(lo, hi, lo_bits, rev_L >= 0 ? brev(i, rev_L) : i) : ld_limbs(c, 0);
   st_packed(a, i, fe_mul<FrCfg>(x, f));
+}
+
+// unpacked table times a constant: out[j] = in[j] * k (< r), j < n  (a post-scale table k * g^(i*e)
+// from the domain's g^(+-i) tables, built on the stream that uses it)
+__global__ void __launch_bounds__(256) k_table_scale(uint32_t* out, const uint32_t* in, uint32_t n, FrConst k) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  DFr c;
+#pragma unroll
+  for (int l = 0; l < 9; l++) c.v[l] = k.v[l];
+  const DFr x = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(ld_limbs(in, j), c));
+#pragma unroll
+  for (int l = 0; l < 9; l++) out[(size_t)j * 9 + l] = x.v[l];
+}
+
+// a = a * k - b  (sub_assign of two domains whose pending constant factors differ)
+__global__ void __launch_bounds__(256) k_scale_sub(uint32_t* a, const uint32_t* b, uint32_t n, FrConst k) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DFr c;
+#pragma unroll
+  for (int l = 0; l < 9; l++) c.v[l] = k.v[l];
+  const DFr x = fe_mul<FrCfg>(ld_packed(a, i), c);
+  st_packed(a, i, fe_csub<FrCfg, 2>(fe_sub<FrCfg, 2>(x, ld_packed(b, i))));
 }
 
 // op 0: a *= b ; op 1: a -= b ; op 2: out = (a*b - c) * k   (H pipeline, prover.rs:221-225)
@@ -370,7 +395,7 @@ void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t
   if (L == 0) {  // one element: a copy, the post-scale and the epilogue
     if (src && src != d) hipMemcpyAsync(d, src, 32, hipMemcpyDeviceToDevice, st);
     if (post_hi) hipLaunchKernelGGL(k_scale, dim3(1), dim3(256), 0, st, d, 1u, post_lo, post_hi, post_lo_bits,
-                                    (const uint32_t*)nullptr);
+                                    (const uint32_t*)nullptr, -1);
     if (epi.kind == NttEpilogue::AB_MINUS_C)
       hipLaunchKernelGGL(k_pointwise, dim3(1), dim3(256), 0, st, epi.pa, epi.pb, (const uint32_t*)d, 1u, 2, epi.k);
     else if (epi.kind == NttEpilogue::SCALARS && epi.n_out)
@@ -404,9 +429,17 @@ void launch_permute(const uint32_t* in, uint32_t* out, int L, const uint32_t* lo
   hipLaunchKernelGGL(k_permute, dim3(nb((size_t)1 << L, 256)), dim3(256), 0, st, in, out, L, lo, hi, lo_bits);
 }
 void launch_scale(uint32_t* a, size_t n, const uint32_t* lo, const uint32_t* hi, int lo_bits, const uint32_t* c,
-                  hipStream_t st) {
+                  hipStream_t st, int rev_L) {
   if (!n) return;
-  hipLaunchKernelGGL(k_scale, dim3(nb(n, 256)), dim3(256), 0, st, a, (uint32_t)n, lo, hi, lo_bits, c);
+  hipLaunchKernelGGL(k_scale, dim3(nb(n, 256)), dim3(256), 0, st, a, (uint32_t)n, lo, hi, lo_bits, c, rev_L);
+}
+void launch_table_scale(uint32_t* out, const uint32_t* in, size_t n, const FrConst& k, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_table_scale, dim3(nb(n, 256)), dim3(256), 0, st, out, in, (uint32_t)n, k);
+}
+void launch_scale_sub(uint32_t* a, const uint32_t* b, size_t n, const FrConst& k, hipStream_t st) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_scale_sub, dim3(nb(n, 256)), dim3(256), 0, st, a, b, (uint32_t)n, k);
 }
 void launch_pointwise(uint32_t* a, const uint32_t* b, const uint32_t* c, size_t n, int op, const uint32_t* k,
                       hipStream_t st) {

@@ -1241,10 +1241,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // the H stream follows the density maps and sorts enqueued so far -- unless the uploading
   // thread is enqueueing H on it vector by vector (bh_prove): those kernels are ordered behind
   // their uploads already, and a wait issued here would land between them at a random point
-  if (!(up && up->on_vector)) {
-    BH_TRY_HIP(hipEventRecord(jev[33], sS));
-    BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
-  }
+  // (jev[33] = the density maps: the small multiexps' stream waits on it below)
+  BH_TRY_HIP(hipEventRecord(jev[33], sS));
+  if (!(up && up->on_vector)) BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
   int big[8], nbig = 0, small[8], nsmall = 0;
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];

@@ -161,6 +161,47 @@ bh_status bh_distribute_powers(bh_ctx* ctx, uint64_t* coeffs, size_t len, const 
 bh_status bh_divide_by_z_on_coset(bh_ctx* ctx, uint64_t* coeffs, uint32_t log_m);
 bh_status bh_mul_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len);
 bh_status bh_sub_assign(bh_ctx* ctx, uint64_t* a, const uint64_t* b, size_t len);
+/* ---- EvaluationDomain with its coefficients resident in HBM (domain.rs:21-190).  The
+ * reference keeps `coeffs` private behind AsRef/AsMut/into_coeffs (domain.rs:21-45), so a
+ * binding can hold them on the device from from_coeffs to into_coeffs: each method below is
+ * an enqueue on the context's stream, and only bh_evdom_read / bh_evdom_into_scalars move
+ * data back.  A handle belongs to its context (free it before the context) and is used by one
+ * thread at a time (the reference's &mut self); different handles of one context may be used
+ * from different threads.
+ *   bh_evdom_from_coeffs   EvaluationDomain::from_coeffs   domain.rs:47-79 (zero-padded to 2^exp;
+ *                          BH_ERR_POLY_DEGREE_TOO_LARGE past 2^31).  `coeffs` (len Montgomery Fr, 4 u64
+ *                          each) is read asynchronously by the context's upload thread, in call
+ *                          order: it stays borrowed until bh_evdom_sync (or read / into_scalars /
+ *                          free) returns
+ *   bh_evdom_fft / _ifft / _coset_fft / _icoset_fft      domain.rs:81-127
+ *   bh_evdom_distribute_powers                           domain.rs:101-113
+ *   bh_evdom_divide_by_z_on_coset                        domain.rs:139-151
+ *   bh_evdom_mul_assign / _sub_assign                    domain.rs:153-189 (lengths must agree:
+ *                          BH_ERR_INVALID_ARGUMENT, where the reference asserts)
+ *   bh_evdom_read          as_ref / into_coeffs: the first len (<= m) coefficients, Montgomery
+ *   bh_evdom_write         as_mut written back: replaces the coefficients by len (<= m) values,
+ *                          zero-padded (asynchronous like from_coeffs)
+ *   bh_evdom_into_scalars  prover.rs:226-231: the first len (<= m) coefficients as canonical
+ *                          scalars (to_le_bits) in a device vector for bh_multiexp_submit_scalars,
+ *                          without leaving the device; consumes the domain (later calls fail with
+ *                          BH_ERR_INVALID_ARGUMENT, free still required) */
+typedef struct bh_evdom bh_evdom;
+bh_status bh_evdom_from_coeffs(bh_ctx* ctx, const uint64_t* coeffs, size_t len, bh_evdom** out);
+bh_status bh_evdom_size(const bh_evdom* d, size_t* m, uint32_t* log_m);
+bh_status bh_evdom_fft(bh_evdom* d);
+bh_status bh_evdom_ifft(bh_evdom* d);
+bh_status bh_evdom_coset_fft(bh_evdom* d);
+bh_status bh_evdom_icoset_fft(bh_evdom* d);
+bh_status bh_evdom_distribute_powers(bh_evdom* d, const uint64_t g_mont[4]);
+bh_status bh_evdom_divide_by_z_on_coset(bh_evdom* d);
+bh_status bh_evdom_mul_assign(bh_evdom* d, bh_evdom* other);
+bh_status bh_evdom_sub_assign(bh_evdom* d, bh_evdom* other);
+bh_status bh_evdom_read(bh_evdom* d, uint64_t* out, size_t len);
+bh_status bh_evdom_write(bh_evdom* d, const uint64_t* coeffs, size_t len);
+bh_status bh_evdom_into_scalars(bh_evdom* d, size_t len, bh_scalars** out);
+bh_status bh_evdom_sync(bh_evdom* d);
+bh_status bh_evdom_free(bh_evdom* d);
+
 /* H block of create_proof: a, b, c hold num_constraints evaluations each (padded to m
  * internally); h_out receives m-1 Montgomery coefficients; *h_len = m-1. */
 bh_status bh_compute_h(bh_ctx* ctx, const uint64_t* a, const uint64_t* b, const uint64_t* c,
