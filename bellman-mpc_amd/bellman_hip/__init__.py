@@ -612,10 +612,13 @@ class ResidentEvaluationDomain:
         self._run(_lib.bh_evdom_sync)
         self._keep = None
 
-    def as_mont(self, n=None):
-        """as_ref (domain.rs:28-32): the first n (default m) coefficients, (n,4) Montgomery."""
+    def as_mont(self, n=None, out=None):
+        """as_ref (domain.rs:28-32): the first n (default m) coefficients, (n,4) Montgomery
+        (into `out` when given: a caller's reused buffer)."""
         n = self.m if n is None else n
-        out = np.zeros((max(n, 1), 4), dtype=np.uint64)
+        if out is None:
+            out = np.zeros((max(n, 1), 4), dtype=np.uint64)
+        assert out.dtype == np.uint64 and out.flags.c_contiguous and out.shape[0] >= n
         self._run(_lib.bh_evdom_read, _ptr(out), n)
         return out[:n]
 

@@ -97,6 +97,31 @@ def main():
         if "k_accumulate_pf<CurveOps<FpOps" in r["Name"]:
             out["trace_g1_accumulate"] = {"calls": int(r["Calls"]), "avg_ms": round(float(r["AverageNs"]) / 1e6, 4),
                                           "source": stats_csv}
+    # the kernel's own time per proof: the union of its dispatch intervals in the kernel trace
+    # (run_kernel_trace.csv beside the stats), per proof of `launches` G1 launches; the first proof
+    # (warmup) is skipped, the median taken -- what bench.py's roofline.avg_launch_ms measures
+    trace_csv = stats_csv.replace("kernel_stats", "kernel_trace")
+    if os.path.exists(trace_csv):
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace_csv))
+                    if "k_accumulate_pf<CurveOps<FpOps" in r["Kernel_Name"])
+        per = int(os.environ.get("G1_LAUNCHES_PER_PROOF", "4"))
+        unions = []
+        for i in range(per, len(iv) - per + 1, per):
+            tot, cs, ce = 0, None, None
+            for a, b in iv[i:i + per]:
+                if cs is None:
+                    cs, ce = a, b
+                elif a <= ce:
+                    ce = max(ce, b)
+                else:
+                    tot += ce - cs
+                    cs, ce = a, b
+            unions.append((tot + ce - cs) / 1e6)
+        if unions:
+            med = sorted(unions)[len(unions) // 2]
+            out["trace_g1_accumulate_union"] = {"per_proof_ms": round(med, 4), "launches_per_proof": per,
+                                                "per_launch_ms": round(med / per, 4), "proofs": len(unions),
+                                                "per_proof_all": [round(u, 3) for u in unions], "source": trace_csv}
     out["notes"] = note
     json.dump(out, open(prefix + "_pmc_2p22.json", "w"), indent=1)
     g = out[G1]
