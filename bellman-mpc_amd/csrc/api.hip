@@ -312,19 +312,8 @@ static Jac<Fp> g1_from_xyzz(const XYZZ<G1F>& p) {
   return xyzz_to_jac(fp_from_dev_g1(p.X), fp_from_dev_g1(p.Y), fp_from_dev_g1(p.ZZ), fp_from_dev_g1(p.ZZZ));
 }
 // window sums -> the multiexp (Horner over the Wb windows, c doublings each; multiexp.rs:244-249),
-// or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction), or
-// the same for each of two bucket halves
+// or, for one shared bucket window, out[0] + 2^shift * out[1] (msm_back's split reduction)
 Jac<Fp> combine_g1(const XYZZ<G1F>* ws, const MsmShape& sh) {
-  if (sh.halves) {  // two bucket halves (reduce_halves_shift)
-    auto dbl_n = [](Jac<Fp> z, int k) {
-      for (int i = 0; i < k; i++) z = jac_dbl(z);
-      return z;
-    };
-    Jac<Fp> lo = jac_add(g1_from_xyzz(ws[0]), dbl_n(g1_from_xyzz(ws[1]), reduce_halves_shift(sh, false, 0)));
-    Jac<Fp> hi = jac_add(g1_from_xyzz(ws[3]), dbl_n(g1_from_xyzz(ws[4]), reduce_halves_shift(sh, false, 1)));
-    hi = jac_add(hi, dbl_n(g1_from_xyzz(ws[5]), reduce_lg2((uint32_t)sh.NB / 2)));
-    return jac_add(lo, hi);
-  }
   const int shift = reduce_split_shift(sh, false);
   if (shift >= 0) {
     Jac<Fp> z = g1_from_xyzz(ws[1]);
@@ -350,16 +339,6 @@ static Jac<bh::Fp2> g2_from_xyzz(const XYZZ<Fp2Ops>& p) {
   return xyzz_to_jac(fp2_from_dev(p.X), fp2_from_dev(p.Y), fp2_from_dev(p.ZZ), fp2_from_dev(p.ZZZ));
 }
 Jac<bh::Fp2> combine_g2(const XYZZ<Fp2Ops>* ws, const MsmShape& sh) {
-  if (sh.halves) {  // two bucket halves (reduce_halves_shift)
-    auto dbl_n = [](Jac<bh::Fp2> z, int k) {
-      for (int i = 0; i < k; i++) z = jac_dbl(z);
-      return z;
-    };
-    Jac<bh::Fp2> lo = jac_add(g2_from_xyzz(ws[0]), dbl_n(g2_from_xyzz(ws[1]), reduce_halves_shift(sh, true, 0)));
-    Jac<bh::Fp2> hi = jac_add(g2_from_xyzz(ws[3]), dbl_n(g2_from_xyzz(ws[4]), reduce_halves_shift(sh, true, 1)));
-    hi = jac_add(hi, dbl_n(g2_from_xyzz(ws[5]), reduce_lg2((uint32_t)sh.NB / 2)));
-    return jac_add(lo, hi);
-  }
   const int shift = reduce_split_shift(sh, true);
   if (shift >= 0) {
     Jac<bh::Fp2> z = g2_from_xyzz(ws[1]);
@@ -502,7 +481,7 @@ bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, c
 }
 
 void ctx_sync_all(bh_ctx* ctx) {
-  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream4d, ctx->bg.cst,
+  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->bg.cst,
                          ctx->bg.st})
     if (st) (void)hipStreamSynchronize(st);
   for (hipStream_t st : ctx->tstream)
@@ -785,52 +764,35 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   }
   int prio_lo = 0, prio_hi = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
-  // side streams (sorts, H pipeline, reduction tails) at high priority; BH_SIDE_PRIORITY=0
-  // puts them at the default priority (A/B experiments)
-  const char* pe = getenv("BH_SIDE_PRIORITY");
-  const int side = (pe && pe[0] == '0') ? prio_lo : prio_hi;
-  // The main stream (the G1 accumulations) at high priority too (BH_MAIN_PRIORITY=0: default
-  // priority, round 4): with the G2 accumulation on a high-priority stream, a G1 workgroup lost every
-  // dispatch race for the register room beside a G2 wave to the sorts' and H's; round-5 rehearsal
-  // with the distributed H unmasked (below): N = 8 10.09-10.11 -> 9.61-9.66 ms per rank, N = 2
-  // 31.4-31.5 -> 31.0-31.1, N = 1 within noise (profiles/r05_ab_sched_N1_2_8.txt).
-  // BH_H_PRIORITY=0 (A/B): the H stream at the default priority.
-  // BH_ACC_PRIORITY=0 (A/B): both accumulation streams (main and the first accumulation's) at the
-  // default priority, below H, the sorts and the tails.
-  const char* me = getenv("BH_MAIN_PRIORITY");
-  const char* he = getenv("BH_H_PRIORITY");
-  const char* ae = getenv("BH_ACC_PRIORITY");
-  const bool acc_lo = ae && ae[0] == '0';
-  const int hprio = (he && he[0] == '0') ? prio_lo : side;
-  if (!(me && me[0] == '0')) {
-    if (!acc_lo) {
-      (void)hipStreamDestroy(c->stream);
-      if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-        release_mask(c); delete c;
-        return BH_ERR_HIP;
-      }
-    }
-    // ... and so must the host -> device copy stream be: with every compute queue at high priority,
-    // a default-priority queue's packets (the copies' completion markers the staging ring waits on)
-    // went unprocessed while the accumulations kept dispatching -- the drop-in's b and c landed at
-    // 33 and 45 ms instead of 7 and 10 (round-5 validation run)
-    (void)hipStreamDestroy(c->h2d);
-    if (hipStreamCreateWithPriority(&c->h2d, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-      release_mask(c); delete c;
-      return BH_ERR_HIP;
-    }
+  // Every stream of a proof at high priority: side streams (sorts, H, reduction tails), the main
+  // stream (the G1 accumulations) too -- with the G2 accumulation on a high-priority stream, a G1
+  // workgroup lost every dispatch race for the register room beside a G2 wave to the sorts' and
+  // H's (round-5 rehearsal: N = 8 10.09-10.11 -> 9.61-9.66 ms per rank, N = 2 31.4-31.5 ->
+  // 31.0-31.1, N = 1 within noise; profiles/r05_ab_sched_N1_2_8.txt).  Accumulation streams below H
+  // and the sorts let H finish ~2 ms earlier in bh_prove but made it 1 ms slower, and the resident
+  // proof too (profiles/r06_ab_acc_priority_dropin.txt).  And so must the host -> device copy
+  // stream be: with every compute queue at high priority, a default-priority queue's packets (the
+  // copies' completion markers the staging ring waits on) went unprocessed while the accumulations
+  // kept dispatching -- the drop-in's b and c landed at 33 and 45 ms instead of 7 and 10.
+  const int side = prio_hi;
+  (void)prio_lo;
+  (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->h2d);
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->h2d, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+    release_mask(c); delete c;
+    return BH_ERR_HIP;
   }
-  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, acc_lo ? prio_lo : side) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, hprio) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess) {
     release_mask(c); delete c;
     return BH_ERR_HIP;
   }
   // The reduction tails run on a quarter of the CUs (every 4th, a CU mask): their waves are
   // latency-bound chains of point additions that would otherwise hold SIMD slots of the
   // accumulations on every CU (same-box A/B at 2^22: -0.5 to -0.8 ms per proof with 64 of 256
-  // CUs; 32 or 96 were no better).  BH_TAIL_CUS = k overrides (0: no mask); BH_SORT_CUS and
-  // BH_H_CUS do the same for the sort and H streams (A/B experiments, default unmasked).
+  // CUs; 32 or 96 were no better).
   // A CU-masked stream takes a hardware queue of its own: only the first live context of a
   // device masks (virtual ranks and extra lanes are further contexts; 8 of them with 8 masked
   // tail queues each oversubscribed the queues and one rank never ran -- a hang).
@@ -838,11 +800,9 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
   c->cu_masked = device >= 0 && device < 64 && g_masked_ctxs[device].fetch_add(1) == 0;
   if (!c->cu_masked && device >= 0 && device < 64) g_masked_ctxs[device].fetch_sub(1);
-  // 1 created, 0 not asked, -1 error; def_k: the CUs the stream gets unless `var` says otherwise
-  auto masked = [&](const char* var, hipStream_t* st, int def_k) -> int {
+  // 1 created, 0 not masked, -1 error; k: the CUs the stream gets
+  auto masked = [&](hipStream_t* st, int k) -> int {
     if (!c->cu_masked) return 0;
-    const char* e = getenv(var);
-    const int k = e ? atoi(e) : def_k;
     if (k <= 0 || ncu <= 0 || k >= ncu) return 0;
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     const int step = ncu / k;
@@ -851,28 +811,16 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
     return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess ? 1 : -1;
   };
   for (auto& t : c->tstream) {
-    const int r = masked("BH_TAIL_CUS", &t, ncu / 4);
+    const int r = masked(&t, ncu / 4);
     if (r < 0 || (r == 0 && hipStreamCreateWithPriority(&t, hipStreamNonBlocking, side) != hipSuccess)) {
       release_mask(c); delete c;
       return BH_ERR_HIP;
     }
   }
-  for (hipStream_t* sp : {&c->stream3, &c->stream4}) {
-    hipStream_t m = nullptr;
-    const int r = masked(sp == &c->stream3 ? "BH_SORT_CUS" : "BH_H_CUS", &m, 0);
-    if (r < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
-    if (r > 0) {
-      (void)hipStreamDestroy(*sp);
-      *sp = m;
-    }
-  }
-  // BH_DIST_H_CUS = k (A/B): the distributed H block (N >= 2 ranks) on a CU-masked stream of k CUs.
-  // Round 3 measured half the CUs better (N = 8: 10.88 -> 10.54 ms per rank) when the accumulations'
-  // stream had the default priority; a masked stream cannot be given high priority
-  // (hipExtStreamCreateWithCUMask), and with every prover stream at high priority (above) the
-  // unmasked H stream4 wins (round 5: N = 8 9.61-9.66 vs 10.09-10.11 ms with half the CUs, N = 2
-  // 31.0-31.1 vs 31.4-31.5; profiles/r05_ab_sched_N1_2_8.txt).  Default: 0, stream4.
-  if (masked("BH_DIST_H_CUS", &c->stream4d, 0) < 0) { release_mask(c); delete c; return BH_ERR_HIP; }
+  // (Masking the sorts, the replicated H or the distributed H -- c->stream4d, half the CUs in round
+  // 3 -- was measured and removed: with every prover stream at high priority the unmasked streams
+  // win, e.g. N = 8 9.61-9.66 against 10.09-10.11 ms per rank with the distributed H on half the
+  // CUs, profiles/r05_ab_sched_N1_2_8.txt.)
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { release_mask(c); delete c; return BH_ERR_HIP; }
   for (auto& e : c->jev)
@@ -899,7 +847,6 @@ __attribute__((visibility("hidden"))) bh_status ctx_create_lane(bh_ctx* primary,
   c->stream2 = primary->stream2;
   c->stream3 = primary->stream3;
   c->stream4 = primary->stream4;
-  c->stream4d = primary->stream4d;
   c->h2d = primary->h2d;
   for (int q = 0; q < bh_ctx::TAIL_STREAMS; q++) c->tstream[q] = primary->tstream[q];
   c->tables = primary->tables;
@@ -972,7 +919,6 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream3);
     (void)hipStreamDestroy(ctx->stream4);
-    if (ctx->stream4d) (void)hipStreamDestroy(ctx->stream4d);
     for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
   }
   const int dev = ctx->device;

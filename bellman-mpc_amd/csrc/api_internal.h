@@ -180,6 +180,9 @@ constexpr size_t TABLE_MIN_USED = (size_t)1 << 16;  // smaller multiexps use pla
 // another proof's multiexps run (a seam caller's Arcs) would hold every HIP call of the process
 // behind them.  take: a buffer of at least `bytes` or null; give: keeps it (bounded) or frees it.
 extern "C" void* scalar_pool_take(int device, size_t bytes, size_t* got);
+// selftest.hip (tests/test_gpu_selftest.py): fe2_mul_sub_kara and the two-product form on
+// caller-chosen operands
+extern "C" bh_status bh_selftest_fp2_mul_sub(int device, const uint32_t* in, size_t n, uint32_t* out);
 struct bh_scalar_buf;
 // a device scalar vector of n canonical scalars (pooled), its ready event created
 extern "C" bh_status new_scalar_buf(bh_ctx* ctx, size_t n, std::shared_ptr<bh_scalar_buf>* out);
@@ -260,7 +263,6 @@ struct bh_ctx {
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
-  hipStream_t stream4d = nullptr; // prover: the distributed H pipeline, CU-masked (first context of a device)
   // prover: reduction-tail streams (high priority, CU-masked on the first context of a device).
   // A proof has at most 5 large multiexps unless the public inputs number in the thousands;
   // more tails share these round robin.  Kept small for the device's hardware-queue budget
@@ -406,7 +408,7 @@ struct Exchanger {
   virtual bh_status exchange(const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec, hipStream_t st) = 0;
 };
 std::unique_ptr<Exchanger> rccl_exchanger(bh_comm* c);
-// smallest rank count that uses the distributed H pipeline (BH_DIST_H_MIN, default 4)
+// smallest rank count that uses the distributed H pipeline (2)
 size_t dist_h_min_ranks();
 // the scratch budget check (scratch.cpp): BH_ERR_SCRATCH_LIMIT when the worst spilling kernel's
 // per-queue scratch times the context's queues exceeds the device's scratch limit (thread-safe;

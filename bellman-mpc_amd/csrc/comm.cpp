@@ -118,14 +118,7 @@ namespace bh {
 // Smallest rank count that distributes the H block.  2: at N = 2 a rank's replicated H (~8 % of
 // the proof's VALU work) was the largest non-shrinking cost; distributing it took the one-GPU
 // rehearsal from 35.2 to 33.7 ms per rank (1.66x -> 1.73x, profiles/r03_ab_dist_h_N2.txt).
-size_t dist_h_min_ranks() {
-  static const size_t v = [] {
-    const char* e = getenv("BH_DIST_H_MIN");
-    const long x = e ? atol(e) : 2;
-    return (size_t)(x > 1 ? x : 2);
-  }();
-  return v;
-}
+size_t dist_h_min_ranks() { return 2; }
 
 static bh_status comm_exchange(bh_comm* c, const uint32_t* send, uint32_t* recv, size_t C, size_t M, int nvec,
                         hipStream_t st) {

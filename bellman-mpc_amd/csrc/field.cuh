@@ -392,9 +392,6 @@ BH_DEV void fe2_mul_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, cons
     }
     acc0 >>= C::BITS;
     acc1 >>= C::BITS;
-#ifdef BH_FP2_COLUMN_SB
-    __builtin_amdgcn_sched_barrier(0);  // one column's products in flight (register pressure)
-#endif
   }
   r1.v[N - 1] = (uint32_t)acc1;
   // r0's top limb is the signed remainder; add p when it is negative
@@ -468,9 +465,6 @@ BH_DEV void fe2_mul_sub_kara(const Fe<C>& a0, const Fe<C>& a1, const Fe<C>& b0, 
     }
     acc0 = (acc0 >> C::BITS) + NEXT;
     acc1 = (acc1 >> C::BITS) + NEXT;
-#ifdef BH_FP2_COLUMN_SB
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   }
   // top limbs: the signed remainders (acc - BIAS); a negative half gets + p
   const int64_t top0 = (int64_t)(acc0 - BIAS), top1 = (int64_t)(acc1 - BIAS);

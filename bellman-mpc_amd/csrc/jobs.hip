@@ -244,18 +244,9 @@ size_t density_set(const uint64_t* density_words, size_t n) {
 // G2 jobs accumulate on the small-multiexp stream (stream2, idle under the seam), so a G2
 // accumulation runs beside the G1 ones as bh_prove's first accumulation does, instead of queueing
 // behind them on the main stream (create_proof submits b_g2_aux last: prover.rs:298-307).
-// BH_JOB_G2_STREAM=0: the main stream (round 4).
-bool job_g2_own_stream() {
-  static const bool v = [] {
-    const char* e = getenv("BH_JOB_G2_STREAM");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 JobStreams job_streams(bh_ctx* ctx, bool g2) {
   static std::atomic<unsigned> rr{0};
-  return JobStreams{ctx->stream3, g2 && job_g2_own_stream() ? ctx->stream2 : ctx->stream,
+  return JobStreams{ctx->stream3, g2 ? ctx->stream2 : ctx->stream,
                     ctx->tstream[rr.fetch_add(1) % bh_ctx::TAIL_STREAMS]};
 }
 

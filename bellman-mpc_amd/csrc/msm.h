@@ -25,11 +25,6 @@ struct MsmShape {
   int Wb;   // bucket windows: W, or 1 with a window table (all windows share the buckets)
   int pre;  // 1: bases are a window table T[i*W + w] = 2^(c*w) * P_i (entry = i*W + w)
   int rec;  // u32 words per base record (0: packed affine, 2 x PACKED_WORDS; see G1_TABLE_REC)
-  // 1 (Wb == 1 only): the bucket set is accumulated and reduced as two halves, each with its own
-  // reduction chain, so the lower half's reduction runs beside the upper half's accumulation
-  // (the prover's last multiexp, msm_back); L2 = buckets per reduction thread of the upper half
-  int halves = 0;
-  int L2 = 0;
   // Bucket shard (Wb == 1 only; bk_hi > bk_lo): only the digits whose bucket lies in
   // [bk_lo, bk_hi) are sorted, accumulated and reduced -- one rank's part of a multiexp split
   // across ranks by bucket range (every rank reads all scalars, the ranks' parts sum to the
@@ -53,7 +48,7 @@ MsmShape msm_shape_table(size_t n, int c);
 // reduce_block_threads() threads.  With a single bucket window (Wb == 1) the device returns
 // two points and the host finishes the window: out[0] + 2^reduce_split_shift() * out[1]
 // (the shift's doublings are a serial chain: cheaper on the host than on one device thread).
-uint32_t reduce_block_max(bool g2);  // BH_REDUCE_BT (A/B), default 256 (G1) / 128 (G2)
+uint32_t reduce_block_max(bool g2);  // 256 (G1) / 128 (G2) threads (64 and 128 were slower)
 // (for a bucket range of nbr buckets, L per thread)
 inline uint32_t reduce_threads_for(uint32_t nbr, uint32_t L, bool g2) {
   const uint32_t T = nbr / L, bmax = reduce_block_max(g2);
@@ -87,16 +82,9 @@ inline void reduce_level2(uint32_t nblk, bool g2, uint32_t* BT2, uint32_t* Lb) {
   *BT2 = t;
   *Lb = lb;
 }
-// halves: out[0..3) is the lower half [0, NB/2): out[0] + 2^shift_lo * out[1]; out[3..6) the
-// upper half, reduced as a window of its own: out[3] + 2^shift_hi * out[4] + (NB/2) * out[5]
-// (out[5] = the plain sum of its buckets, each of which holds digit NB/2 more than its position)
-inline int reduce_halves_shift(const MsmShape& sh, bool g2, int upper) {
-  return reduce_shift_for((uint32_t)sh.NB / 2, (uint32_t)(upper ? sh.L2 : sh.L), g2);
-}
 
 struct MsmTiming {
   hipEvent_t ev_acc_begin = nullptr, ev_acc_end = nullptr;  // bracket k_accumulate_dev
-  hipEvent_t ev_half = nullptr;  // halves: recorded once the lower half is accumulated
 };
 
 // G2 window-table record: raw-limb x, y (4 x 14 limbs, 56 words) in a 256-B line
@@ -135,12 +123,11 @@ template <class C>
 void fit_segments(MsmShape& sh, size_t n);
 template <class C>
 void fit_segments_E(MsmShape& sh, size_t E);  // the same for E expected entries
-// The entries fit_segments sizes a multiexp's segments for: n * W for n scalars and W windows
-// (default), or used * W with BH_SEG_USED=1 (`used` = the density set's scalars).  With n * W a
-// half-density multiexp (b_g1_aux, b_g2_aux) gets segments for twice its entries, i.e. half its
-// rounds (1.5 at the 3-round default): alone its last round is half empty (G2 17.2 against 13.4 ms),
-// but in the overlapped proof that is 1.1 ms per 2^22 proof faster than sizing every multiexp for
-// its own entries (profiles/r05_ab_seg_used.txt).
+// The entries fit_segments sizes a multiexp's segments for: n * W for n scalars and W windows,
+// not used * W (`used` = the density set's scalars).  So a half-density multiexp (b_g1_aux,
+// b_g2_aux) gets segments for twice its entries, i.e. half its rounds (1.5 at 3 rounds): alone its
+// last round is half empty (G2 17.2 against 13.4 ms), but in the overlapped proof that is 1.1 ms
+// per 2^22 proof faster than sizing it for its own entries (profiles/r05_ab_seg_used.txt).
 size_t seg_entries(size_t n, size_t used, int W);
 template <class C>
 hipError_t msm_sort(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_scalars, size_t n, const int32_t* d_idx,
@@ -154,8 +141,6 @@ hipError_t msm_front(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d_base
 // max_span: the largest number of continuation partials of one bucket (max_span() below)
 // when known, so that only the continuation-tree levels that can do work are launched;
 // -1: every level a bucket could need
-// halves: the caller orders `st` after the lower half (MsmTiming::ev_half); msm_back enqueues
-// the lower half's reduction, waits for `acc_done` (the whole accumulation), then the upper's
 // d_span_words (with max_span = -1): max_span()'s device words for this multiexp -- the kernels
 // read the longest span themselves (fold in the reduction up to 8 segments, else k_cont_seq),
 // so the host need not wait for the sort before enqueueing the tail

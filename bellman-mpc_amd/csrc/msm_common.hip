@@ -211,6 +211,9 @@ __device__ __forceinline__ void load_scalar(const uint32_t* scalars, size_t i, u
 // {c-1, c, c+1} whose top window is fullest (a nearly empty top window piles
 // every scalar into a handful of giant buckets).  Segment length S keeps about
 // 2^18 accumulation threads in flight.  Results never depend on either choice.
+// minimum bucket-reduction threads: a small bucket set's tail is latency-bound
+static constexpr size_t REDUCE_T_MIN = 16384;
+
 MsmShape msm_shape(size_t n, int c_override) {
   MsmShape sh;
   int c = c_override;
@@ -235,17 +238,8 @@ MsmShape msm_shape(size_t n, int c_override) {
   // proof in a same-box A/B), fewer when that leaves under 16384 threads (a small bucket set's
   // tail is latency-bound: a shard's G2 tail at 2^15 buckets took 5.8 ms beside the
   // accumulations with L = 8, 4096 threads)
-  static const int l_big = [] {  // BH_REDUCE_L: the large-set value (A/B experiments)
-    const char* e = getenv("BH_REDUCE_L");
-    const int v = e ? atoi(e) : 8;
-    return (v >= 1 && v <= 64 && (v & (v - 1)) == 0) ? v : 8;
-  }();
-  static const size_t t_min = [] {  // BH_REDUCE_TMIN: minimum reduction threads
-    const char* e = getenv("BH_REDUCE_TMIN");
-    return e ? (size_t)atol(e) : (size_t)16384;
-  }();
-  sh.L = std::min<int>(l_big, sh.NB);
-  while (sh.L > 1 && (size_t)sh.W * (size_t)(sh.NB / sh.L) < t_min) sh.L >>= 1;
+  sh.L = std::min<int>(8, sh.NB);
+  while (sh.L > 1 && (size_t)sh.W * (size_t)(sh.NB / sh.L) < REDUCE_T_MIN) sh.L >>= 1;
   size_t E = n * (size_t)sh.W;
   int S = 16;
   while (S < 256 && E / (size_t)(2 * S) >= ((size_t)1 << 18)) S <<= 1;
@@ -266,32 +260,18 @@ MsmShape msm_shape(size_t n, int c_override) {
 // nearly empty top window (e.g. c = 17: the 16th window only takes the carry; c = 18: 3 bits)
 // pours up to n/2 entries into a handful of small-digit buckets, whose continuation partials
 // then need the log-depth tree (msm_back).  For 255-bit scalars: c = 16, 20, 22, 24.
-uint32_t reduce_block_max(bool g2) {
-  static const uint32_t v = [] {
-    const char* e = getenv("BH_REDUCE_BT");
-    const long x = e ? atol(e) : 0;
-    return (x == 64 || x == 128 || x == 256) ? (uint32_t)x : 0u;
-  }();
-  if (v) return g2 ? std::min<uint32_t>(v, 128u) : v;
-  return g2 ? 128u : 256u;
-}
+uint32_t reduce_block_max(bool g2) { return g2 ? 128u : 256u; }
 
+// Entries the accumulation grid is sized for: n * W, the query's full length even where a density
+// map leaves about half of it (b_g1_aux, b_g2_aux).  Sized for the used entries, b_g2_aux alone is
+// 13.4 against 17.2 ms, but the overlapped 2^22 proof is 1.1-1.3 ms slower: the longer segments
+// leave room beside it for the G1 accumulations (profiles/r05_ab_seg_used.txt).
 size_t seg_entries(size_t n, size_t used, int W) {
-  static const bool by_used = [] {
-    const char* e = getenv("BH_SEG_USED");
-    return e && e[0] == '1';
-  }();
-  const size_t k = by_used ? std::min(used, n) : n;
-  return std::max<size_t>(k, 1) * (size_t)std::max(W, 1);
+  (void)used;
+  return std::max<size_t>(n, 1) * (size_t)std::max(W, 1);
 }
 
 int msm_table_c(size_t n) {
-  static const int forced = [] {  // BH_TABLE_C: force the table window size (A/B experiments)
-    const char* e = getenv("BH_TABLE_C");
-    const int v = e ? atoi(e) : 0;
-    return (v == 16 || v == 20 || v == 22 || v == 24) ? v : 0;
-  }();
-  if (forced) return forced;
   int best = 16;
   double best_cost = 1e300;
   for (int c = 8; c <= 24; c++) {
@@ -308,11 +288,7 @@ MsmShape msm_shape_table(size_t n, int c) {
   sh.Wb = 1;
   sh.pre = 1;
   // one shared bucket window: the reduction's thread count is NB / L
-  static const size_t t_min = [] {
-    const char* e = getenv("BH_REDUCE_TMIN");
-    return e ? (size_t)atol(e) : (size_t)16384;
-  }();
-  while (sh.L > 1 && (size_t)(sh.NB / sh.L) < t_min) sh.L >>= 1;
+  while (sh.L > 1 && (size_t)(sh.NB / sh.L) < REDUCE_T_MIN) sh.L >>= 1;
   return sh;
 }
 

@@ -1,9 +1,5 @@
 // G1Ops instantiation of the device MSM, part 1: workspace, digit sort and the bucket
 // accumulation kernels (see msm_impl.cuh).
-// BH_G1_ACC_WAVES (A/B): register budget of the G1 accumulation as waves per SIMD
-#ifdef BH_G1_ACC_WAVES
-#define BH_ACC_REGS_ATTR __attribute__((amdgpu_waves_per_eu(BH_G1_ACC_WAVES)))
-#endif
 #include "msm_impl.cuh"
 
 namespace bh {

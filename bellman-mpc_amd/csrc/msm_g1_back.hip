@@ -1,13 +1,5 @@
 // G1Ops instantiation of the device MSM, part 2: continuation fix-up, bucket reduction
 // and window sums (see msm_impl.cuh).
-// BH_BACK_ALL_REGS (A/B): the reduction kernels (one wave per SIMD) may use AGPRs as well
-#ifdef BH_BACK_ALL_REGS
-#define BH_BACK_REGS_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
-#endif
-// BH_G1_BACK_WAVES (A/B): the G1 reduction kernels at this many waves per SIMD
-#ifdef BH_G1_BACK_WAVES
-#define BH_BACK_REGS_ATTR __attribute__((amdgpu_waves_per_eu(BH_G1_BACK_WAVES)))
-#endif
 #include "msm_impl.cuh"
 
 namespace bh {

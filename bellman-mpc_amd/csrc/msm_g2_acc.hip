@@ -2,10 +2,6 @@
 // accumulation kernels (see msm_impl.cuh).  The accumulation's Fp2 products use the column-wise
 // Karatsuba form (field.cuh); every kernel of this unit is emitted here only.
 #define BH_FP2_KARATSUBA 1
-// BH_G2_ACC_ALL_REGS (A/B): the G2 accumulation (one wave per SIMD) may use AGPRs as well
-#ifdef BH_G2_ACC_ALL_REGS
-#define BH_ACC_REGS_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
-#endif
 #include "msm_impl.cuh"
 
 namespace bh {

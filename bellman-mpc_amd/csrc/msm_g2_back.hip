@@ -1,9 +1,5 @@
 // G2Ops instantiation of the device MSM, part 2: continuation fix-up, bucket reduction
 // and window sums (see msm_impl.cuh).
-// BH_BACK_ALL_REGS (A/B): the reduction kernels (one wave per SIMD) may use AGPRs as well
-#ifdef BH_BACK_ALL_REGS
-#define BH_BACK_REGS_ATTR __attribute__((amdgpu_waves_per_eu(1, 1)))
-#endif
 #include "msm_impl.cuh"
 
 namespace bh {

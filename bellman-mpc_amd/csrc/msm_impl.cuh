@@ -6,16 +6,6 @@
 #include "msm.h"
 #include <algorithm>
 
-// Register budget of the kernels a translation unit instantiates: a kernel that runs one wave per
-// SIMD anyway (G2 accumulation, every bucket reduction) may use the whole 512-register file of a
-// lane (256 VGPRs + 256 AGPRs), so the allocator parks values in AGPRs instead of spilling to
-// scratch.  Empty = the compiler's default (G1 accumulation: two waves per SIMD).
-#ifndef BH_ACC_REGS_ATTR
-#define BH_ACC_REGS_ATTR
-#endif
-#ifndef BH_BACK_REGS_ATTR
-#define BH_BACK_REGS_ATTR
-#endif
 
 namespace bh {
 
@@ -72,7 +62,7 @@ __device__ __forceinline__ typename C::P bucket_value(uint32_t gb, const uint32_
 // partials at j + i*stride, i = 1..F-1 (F-1 serial additions per level instead of one per
 // level of the binary tree).  After the levels with stride < span, conts[s_first+1] holds the sum.
 template <class C, int F>
-__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
+__global__ void __launch_bounds__(256) k_cont_treeF(const uint32_t* cont_bucket, const uint32_t* counts,
                                                     const uint32_t* offsets, uint32_t nbt, uint32_t S,
                                                     uint32_t stride, uint32_t b_lo, uint32_t b_hi,
                                                     typename C::P* conts) {
@@ -95,14 +85,8 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_treeF(const uint
 // longest span folded by the Q-thread kernel below; longer ones take the 4-ary tree.  The
 // tree's levels are full-grid launches: beside a running accumulation they cost more than a
 // sequential fold of ~16 partials (N = 8 rehearsal at 2^22: 13.4 ms per rank with 4, 10.7 ms
-// with 24).  BH_CONT_SEQ_MAX: A/B experiments.
-inline size_t cont_seq_max() {
-  static const size_t v = [] {
-    const char* e = getenv("BH_CONT_SEQ_MAX");
-    return e ? (size_t)atol(e) : (size_t)64;
-  }();
-  return v;
-}
+// with 24).
+inline size_t cont_seq_max() { return 64; }
 
 // Max over the g per-workgroup words k_max_span wrote (msm_common.hip): the longest bucket span,
 // read by every workgroup of the kernels below when the host has not read it (device-decided
@@ -131,7 +115,7 @@ __device__ __forceinline__ uint32_t block_span(const uint32_t* words, uint32_t g
 // seq_max segments; longer ones are k_cont_long's (a serial chain over thousands of partials
 // would be the tail's latency: a witness full of ones puts most entries in one bucket).
 template <class C, int Q>
-__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
+__global__ void __launch_bounds__(256) k_cont_seq(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
                                                   uint32_t nbr, uint32_t S, typename C::P* conts,
                                                   const uint32_t* span_words, uint32_t span_g, uint32_t fold_span,
                                                   uint32_t seq_max) {
@@ -170,7 +154,7 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_seq(const uint32
 // partials, then an LDS tree, into conts[s_first+1].  A grid-stride pass over the buckets finds
 // them; the whole grid returns at once when the longest span is at most seq_max.
 template <class C>
-__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_cont_long(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
+__global__ void __launch_bounds__(256) k_cont_long(const uint32_t* counts, const uint32_t* offsets, uint32_t b0,
                                                    uint32_t nbr, uint32_t S, typename C::P* conts,
                                                    const uint32_t* span_words, uint32_t span_g, uint32_t seq_max) {
   extern __shared__ uint4 lds_raw[];
@@ -309,7 +293,7 @@ __device__ __forceinline__ void block_epilogue(typename C::P v, const typename C
 // they are all added here (short spans), else k_cont_seq / k_cont_treeF has already folded
 // them into conts[s_first+1].
 template <class C>
-__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
+__global__ void __launch_bounds__(256) k_reduce_blocks(const uint32_t* counts, const uint32_t* offsets,
                                                        const typename C::P* bucket_sums, const typename C::P* conts,
                                                        uint32_t S, uint32_t b0, uint32_t NB, uint32_t L, int lgL,
                                                        uint32_t nblk, int fold, typename C::P* Y, typename C::P* Ssum,
@@ -323,11 +307,7 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_blocks(const u
   // G2 (448-byte points, one wave per SIMD): the running total `acc` waits in this thread's LDS
   // slot (free until the epilogue) instead of registers, which the compiler otherwise spills
   // to scratch (KB per lane)
-#ifdef BH_G1_REDUCE_LDS
-  constexpr bool acc_lds = true;
-#else
   constexpr bool acc_lds = sizeof(typename C::P) > 256;
-#endif
   typename C::P run = C::identity(), acc = C::identity(), bk = C::identity();
   if (acc_lds) store_point<C>(&lds[i], acc);
   // per bucket k = L-1 .. 0:  bk = partial (+ each continuation partial);  run += bk;  acc += run
@@ -384,7 +364,7 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_blocks(const u
 // out[1] = sum_blk blk * S, out[2] = sum_blk S, and the host adds 2^lgM * out[1]
 // (reduce_split_shift; out[2] is the plain bucket sum a bucket range's offset multiplies).
 template <class C>
-__global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
+__global__ void __launch_bounds__(256) k_reduce_window(const typename C::P* Y, const typename C::P* Ssum,
                                                        uint32_t nblk, uint32_t Lb, int lgLb, int lgM, int split,
                                                        typename C::P* out) {
   extern __shared__ uint4 lds_raw[];
@@ -430,11 +410,7 @@ __global__ void __launch_bounds__(256) BH_BACK_REGS_ATTR k_reduce_window(const t
 // in the loop took the kernel back to 512 registers with scratch spills; out of line it needs a
 // call stack: scratch in the hot kernel).  Identity is a register flag.
 // Bounds as CurveOps::madd (MB = 2: X < 10p, Y < 4p, ZZ, ZZZ < 2p).
-#ifndef BH_G2_NO_SB
 #define G2_SB() __builtin_amdgcn_sched_barrier(0)
-#else
-#define G2_SB()
-#endif
 // DIRECT: no LDS prefetch slots (pre unused): each coordinate of the base is loaded from `bases`
 // when it is needed, and the other wave of the SIMD covers the latency (two waves per SIMD: 57 KB
 // of LDS per 256-thread block instead of 114).
@@ -620,15 +596,11 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
     const T X3 = F::template sub<Cv::K1>(F::sqr(R), twice ? Q2 : F::add(PPP, Q2));
     G2_SB();
     if constexpr (std::is_same<F, Fp2Ops>::value) {
-#ifndef BH_G2_Y3_TWO_PRODUCTS
       // one reduction per half for both Karatsuba products (fe2_mul_sub_kara): R < 6p,
       // Q - X3 + 16p < 18p, Y < 4p, PPP < 2p, all < 2^386 with normalised limbs; Y3 < 2p
+      // (round 5: two products and a subtraction before, 14 761 against 14 038 VALU lane-
+      // instructions per madd; checked at the operand maxima by tests/test_gpu_selftest.py)
       Y = F::mul_sub_lazy(R, F::template sub<Cv::K2>(Q, X3), Y, PPP);
-#else  // (A/B) two products, one at a time, then a subtraction: < 4p
-      const T RQ3 = F::mul(R, F::template sub<Cv::K2>(Q, X3));
-      G2_SB();
-      Y = F::template sub<2>(RQ3, F::mul(Y, PPP));
-#endif
     } else {  // one reduction for both products (fe_mul2)
       Y = F::template mul_sub<Cv::KY>(R, F::template sub<Cv::K2>(Q, X3), Y, PPP);
     }
@@ -645,11 +617,11 @@ __device__ __forceinline__ void accumulate_lds(uint4 (*pre)[64], int lane, int n
 // segment.  The next entry's affine base is prefetched global -> LDS by
 // global_load_lds_dwordx4 (no VGPR cost) while the current mixed addition runs: each wave
 // owns NQ x 64 x 16 B of LDS, lane l's base occupying slot l of each of the NQ rows.
-// Only the entries of buckets [b_lo, b_hi) (MsmShape::halves: two launches); a segment cut by
-// the range keeps the continuation bookkeeping of the whole segment.
+// Only the entries of buckets [b_lo, b_hi) (a bucket shard's range); a segment cut by the range
+// keeps the continuation bookkeeping of the whole segment.
 // (A register-load variant without the prefetch measured slower and was removed.)
 template <class C>
-__global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
+__global__ void __launch_bounds__(256) k_accumulate_pf(const uint32_t* entries, const uint32_t* offsets, uint32_t nbt,
                                                        const uint32_t* bases, uint32_t rec, uint32_t S,
                                                        uint32_t b_lo, uint32_t b_hi, typename C::P* bucket_sums,
                                                        typename C::P* conts, uint32_t* cont_bucket) {
@@ -687,20 +659,12 @@ __global__ void __launch_bounds__(256) BH_ACC_REGS_ATTR k_accumulate_pf(const ui
   uint32_t next = offsets[b + 1];
   bool started_here = offsets[b] >= pos0;
   if (start == pos0) cont_bucket[seg] = started_here ? 0xffffffffu : b;
-#ifndef BH_G2_ACC_REGS
   if constexpr (!G1) {
     accumulate_lds<F, NW, NQ, true>(pre[wv], lane, nq, limbs, entries, offsets, start, end, pos0, seg, b, next,
                                     started_here, e_cur, e_next, issue, bucket_sums, conts);
     return;
   }
-#endif
-#ifdef BH_G1_ACC_LDS  // (A/B) G1 through the same loop: ZZZ in LDS (BH_G1_ACC_LDS=2: ZZ too)
-  if constexpr (G1) {
-    accumulate_lds<F, NW, NQ, BH_G1_ACC_LDS == 2>(pre[wv], lane, nq, limbs, entries, offsets, start, end, pos0, seg,
-                                                  b, next, started_here, e_cur, e_next, issue, bucket_sums, conts);
-    return;
-  }
-#endif
+  // (G1 through the same loop with ZZZ, or ZZ and ZZZ, in LDS: no faster, removed in round 6)
   typename C::P acc = C::identity();
   for (uint32_t j = start; j < end; j++) {
     if (j == next) {
@@ -812,32 +776,13 @@ void fit_segments_E(MsmShape& sh, size_t E) {
   // 53.4-53.9 with 2, 58.5-59.4 with 1, and the rehearsal faster at N = 1, 2 and 8 too
   // (profiles/r05_ab_acc_rounds.txt): fewer segments are fewer continuation partials and bucket
   // stores, and with the G2 and G1 accumulations sharing the SIMDs a third round balances the
-  // finish well enough.  BH_ACC_ROUNDS (BH_ACC_ROUNDS_G1 / BH_ACC_ROUNDS_G2: one group only)
-  static const double rounds = [] {  // (fractional values allowed: A/B)
-    const char* e = getenv(std::is_same<C, G1Ops>::value ? "BH_ACC_ROUNDS_G1" : "BH_ACC_ROUNDS_G2");
-    if (!e) e = getenv("BH_ACC_ROUNDS");
-    const double r = e ? atof(e) : 3.0;
-    return r > 0.0 ? r : 3.0;
-  }();
-  // BH_ACC_FILL: fraction of the resident capacity the accumulation occupies per round
-  // (the rest stays free for the side streams' short kernels)
-  // (BH_ACC_FILL_G1 / BH_ACC_FILL_G2: the same for one group only)
-  static const double fill = [] {
-    const char* e = getenv(std::is_same<C, G1Ops>::value ? "BH_ACC_FILL_G1" : "BH_ACC_FILL_G2");
-    if (!e) e = getenv("BH_ACC_FILL");
-    const double f = e ? atof(e) : 1.0;
-    return (f > 0.0 && f <= 1.0) ? f : 1.0;
-  }();
-  // BH_ACC_MIN_S: floor of the segment length (short segments multiply the continuation
-  // partials and the per-segment bucket search)
-  static const size_t min_s = [] {
-    const char* e = getenv("BH_ACC_MIN_S");
-    const long v = e ? atol(e) : 8;
-    return (size_t)(v >= 1 ? v : 8);
-  }();
-  const size_t slots = std::max<size_t>((size_t)(rounds * (double)conc * fill) / 256 * 256, 256);
+  // finish well enough.  Round 6: 2, 1.5, 4 and 6 rounds (G1, G2 or both) no better at N = 1, 4
+  // and 8 or for bh_prove (profiles/r06_ab_acc_rounds.txt).  Segments of at least 8 entries
+  // (shorter ones multiply the continuation partials and the per-segment bucket search).
+  constexpr size_t ROUNDS = 3, MIN_S = 8;
+  const size_t slots = std::max<size_t>(ROUNDS * conc / 256 * 256, 256);
   size_t S = (E + slots - 1) / slots;
-  sh.S = (int)std::min<size_t>(std::max<size_t>(S, min_s), (size_t)1 << 16);
+  sh.S = (int)std::min<size_t>(std::max<size_t>(S, MIN_S), (size_t)1 << 16);
 }
 
 template <class C>
@@ -985,7 +930,6 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
     if (timing && timing->ev_acc_begin) hipEventRecord(timing->ev_acc_begin, st);
     using F = typename std::conditional<std::is_same<C, G1Ops>::value, G1F, Fp2Ops>::type;
     const uint32_t rec = sh.rec ? (uint32_t)sh.rec : 2u * F::PACKED_WORDS;
-    const uint32_t cut = sh.halves ? (uint32_t)(sh.NB / 2) : (uint32_t)nbt;
     if (sh.bucket_shard()) {  // only the shard's buckets are sorted (their offsets alone are set)
       launch_range_first = sh.bk_lo;
       launch_range_end = sh.bk_hi;
@@ -1004,11 +948,7 @@ hipError_t msm_accumulate(MsmWorkspace<C>& ws, hipStream_t st, const uint32_t* d
                          ws.cont_bucket);
     };
     if (sh.bucket_shard()) launch(launch_range_first, launch_range_end);
-    else launch(0u, cut);
-    if (sh.halves) {
-      if (timing && timing->ev_half) hipEventRecord(timing->ev_half, st);
-      launch(cut, (uint32_t)nbt);
-    }
+    else launch(0u, (uint32_t)nbt);
     if (timing && timing->ev_acc_end) hipEventRecord(timing->ev_acc_end, st);
   }
   return hipGetLastError();
@@ -1086,17 +1026,14 @@ static void reduce_range(MsmWorkspace<C>& ws, const AccView& v, hipStream_t st, 
 }
 
 // Back half: continuation fix-up, summation by parts and the per-window sums, copied to host_out
-// (Wb entries; 2 for one shared window; 6 for halves, see reduce_halves_shift).
+// (Wb entries; 2 for one shared window, 3 for a bucket shard).
 template <class C>
 hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShape& sh, typename C::P* host_out,
                     int max_span, hipEvent_t acc_done, const uint32_t* d_span_words) {
   // continuation partials: a bucket spanning up to REDUCE_FOLD_SPAN segments has them added
   // by its reduction thread (no extra launch); longer spans (known from the sort) are folded
   // first -- Q threads per bucket, or log-depth 4-ary tree levels
-  static const size_t REDUCE_FOLD_SPAN = [] {  // BH_FOLD_SPAN: A/B experiments
-    const char* e = getenv("BH_FOLD_SPAN");
-    return e ? (size_t)atol(e) : (size_t)8;
-  }();
+  constexpr size_t REDUCE_FOLD_SPAN = 8;
   const AccView v = acc_view<C>(ws, n, sh);
   const size_t segs = (v.E + v.S - 1) / v.S;
   const size_t span = max_span >= 0 ? (size_t)max_span : segs;
@@ -1109,15 +1046,7 @@ hipError_t msm_back(MsmWorkspace<C>& ws, hipStream_t st, size_t n, const MsmShap
     dev.fold_span = (uint32_t)REDUCE_FOLD_SPAN;
     dev.seq_max = (uint32_t)cont_seq_max();
   }
-  if (sh.halves) {
-    const uint32_t nbh = (uint32_t)sh.NB / 2;
-    reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, 0, nbh, (uint32_t)sh.L, 0, ws.window_sums, dev);
-    if (acc_done) hipStreamWaitEvent(st, acc_done, 0);
-    const uint32_t y_off = nbh / sh.L / reduce_threads_for(nbh, (uint32_t)sh.L, sizeof(typename C::P) > 256);
-    reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, nbh, nbh, (uint32_t)sh.L2, y_off, ws.window_sums + 3, dev);
-    hipMemcpyAsync(host_out, ws.window_sums, 6 * sizeof(typename C::P), hipMemcpyDeviceToHost, st);
-    return hipGetLastError();
-  }
+  (void)acc_done;  // (stream order: the caller's st already follows the accumulation)
   reduce_range<C>(ws, v, st, sh, segs, span, fold, seq, sh.red_lo(), sh.red_nb(), (uint32_t)sh.L, 0, ws.window_sums,
                   dev);
   const int outs = sh.bucket_shard() ? 3 : (sh.Wb == 1 ? 2 : sh.Wb);

@@ -102,14 +102,8 @@ __device__ __forceinline__ uint32_t dit_index(const PassArgs& a, uint32_t g, uin
 // (consecutive groups) read consecutive entries, and the level-0 stage (h = 1: every twiddle
 // is 1) multiplies by nothing.  Entries are stored as the 9 limbs (36 bytes, L2-resident at
 // the sizes that matter): an unpack per twiddle (~25 VALU) costs more than the 4 extra bytes.
-// BH_NTT_WAVES (A/B build): register budget as waves per SIMD (LDS allows 4 workgroups per CU)
-#ifdef BH_NTT_WAVES
-#define BH_NTT_ATTR __attribute__((amdgpu_waves_per_eu(BH_NTT_WAVES)))
-#else
-#define BH_NTT_ATTR
-#endif
 template <bool DIF>
-__global__ void __launch_bounds__(NTT_T) BH_NTT_ATTR k_ntt_pass(uint32_t* data, PassArgs a) {
+__global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) {
   __shared__ uint32_t lds[9 * NTT_E];
   const int D = a.D;
   const int lgG = NTT_LG_E - D;

@@ -142,15 +142,11 @@ bh_status witness_host(bh_ctx* ctx, bh_witness* w, const uint64_t* a, const uint
   return BH_OK;
 }
 
-// Caller (pageable) bytes -> device on the copy stream st.  Default: the pinned staging ring
-// (memcpy workers + DMA).  BH_UPLOAD_DIRECT=1: one hipMemcpyAsync from the pageable buffer (the
-// runtime's own staging; 56 GB/s in tools/microbench/h2dbench.cpp against ~50 for the ring, A/B).
+// Caller (pageable) bytes -> device on the copy stream st: the pinned staging ring (memcpy
+// workers + DMA).  (One hipMemcpyAsync from the pageable buffer -- the runtime's own staging, 56
+// GB/s in tools/microbench/h2dbench.cpp against ~50 for the ring -- was within noise for bh_prove,
+// profiles/r05_ab_dropin_h_uploader.txt, and removed.)
 hipError_t upload_host(bh_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t st) {
-  static const bool direct = [] {
-    const char* e = getenv("BH_UPLOAD_DIRECT");
-    return e && e[0] == '1';
-  }();
-  if (direct) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
   return ctx->ring.copy(ctx_pool(ctx), dst, src, bytes, st);
 }
 
@@ -402,17 +398,13 @@ bool bucket_shards_use(int device, size_t na, size_t nshards, int co_ranks) {
 }
 
 // Rank `shard` of N: its bucket range [lo, hi), granule-aligned, balancing the expected
-// accumulation (used * bucket_cdf) plus the reduction (BH_SHARD_BUCKET_W = 3 additions per
-// bucket).  False when the bucket set is too small to give every rank several granules.
+// accumulation (used * bucket_cdf) plus the reduction (3 additions per bucket).  False when the bucket set is too small to give every rank several granules.
 bool bucket_shard_range(int c, size_t used, size_t shard, size_t N, uint32_t* lo, uint32_t* hi) {
   const int W = (256 + c - 1) / c;
   const uint32_t NB = 1u << (c - 1);
   const uint32_t G = std::max<uint32_t>(BUCKET_SHARD_GRANULE, NB >> 12);  // (sort partition width)
   if ((size_t)NB < 4 * N * G) return false;
-  const double kw = [] {
-    const char* e = getenv("BH_SHARD_BUCKET_W");
-    return e ? atof(e) : 3.0;
-  }();
+  constexpr double kw = 3.0;
   auto cost = [&](double b) { return (double)used * bucket_cdf(c, W, b) + kw * b; };
   const double total = cost(NB);
   auto bound = [&](size_t k) -> uint32_t {
@@ -489,12 +481,9 @@ bh_status ensure_table(bh_ctx* ctx, bh_srs* srs, int c, size_t lo, size_t hi) {
 
 // BH_ACC_EVENTS=0: no timing events around the accumulations (A/B of their cost; the
 // accumulation timings of bh_last_timings then read 0)
-bool acc_events_on() {
-  static const bool v = [] {
-    const char* e = getenv("BH_ACC_EVENTS");
-    return !(e && e[0] == '0');
-  }();
-  return v;
+bool acc_events_on() {  // (read per proof: tests/test_gpu_parity.py runs both modes)
+  const char* e = getenv("BH_ACC_EVENTS");
+  return !(e && e[0] == '0');
 }
 
 // One multiexp of create_proof (prover.rs:233-307) as planned for a shard.
@@ -686,14 +675,7 @@ bh_status plan_shard(bh_ctx* ctx, const bh_params* params_c, const bh_witness* w
                w->b_in_total);                                                                         // b_g2_aux
   jobs[1] = mk(false, &params->b_g1, aux, na, idx_baux, w->b_aux_total, 5, &w->b_aux_density, &w->b_aux_prefix,
                w->b_in_total);                                                                         // b_g1_aux
-  // BH_G1_FIRST=1 (A/B): b_g1_aux sorted and accumulated first, b_g2_aux copying its sort second --
-  // a G2 accumulation wave takes a SIMD's whole register file, so nothing (e.g. a distributed H's
-  // passes) can share its SIMDs, while a G1 accumulation (2 x 180 VGPRs) leaves room for one
-  static const bool g1_first = [] {
-    const char* e = getenv("BH_G1_FIRST");
-    return e && e[0] == '1';
-  }();
-  if (g1_first) std::swap(jobs[0], jobs[1]);
+  // (b_g1_aux first, b_g2_aux copying its sort: N = 8 +0.2 ms per rank, r03_ab_g1_first.txt; removed)
   jobs[2] = mk(false, &params->l, aux, na, nullptr, na, 1, nullptr, nullptr, 0);                       // l
   jobs[3] = mk(false, &params->a, aux, na, idx_aaux, w->a_aux_total, 3, &w->a_aux_density, &w->a_aux_prefix,
                ni);                                                                                    // a_aux
@@ -775,25 +757,10 @@ bh_status prepare_tables_full(bh_ctx* ctx, bh_params* params, size_t m, size_t n
   return full(&params->b_g2, b_aux_used);
 }
 
-// bh_prove's H block reads the uploaded bls12_381-Montgomery a, b, c in place instead of converting
-// them first (BH_H_FUSED_CONVERT=0: the conversion kernel, round 5's first scheme).  Beside the
-// accumulations each extra kernel on the H stream waits for free slots: the round-5 drop-in trace
-// showed a's conversion (a trivial kernel) taking 9.5 ms to get through.
-bool h_fused_convert() {
-  static const bool v = [] {
-    const char* e = getenv("BH_H_FUSED_CONVERT");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 // BH_PROVER_SERIAL=1: one stream (per-kernel profiling only)
-bool prover_serial() {
-  static const bool serial = [] {
-    const char* e = getenv("BH_PROVER_SERIAL");
-    return e && e[0] == '1';
-  }();
-  return serial;
+bool prover_serial() {  // (read per proof: tests/test_gpu_parity.py runs both modes)
+  const char* e = getenv("BH_PROVER_SERIAL");
+  return e && e[0] == '1';
 }
 
 // resident threads of the G1 bucket reduction (k_reduce_blocks) on every CU (full) or on the
@@ -898,15 +865,11 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   }
   // The last multiexp's reduction tail runs when every accumulation is done, alone at the end of
   // the critical path: on the CU-masked tail streams (a quarter of the CUs) its 2^19-bucket
-  // reduction needed two rounds of resident blocks.  BH_LAST_TAIL_FULL (default on, not on a
-  // pipelined batch lane, whose next proof's first accumulation would queue behind it): on the
+  // reduction needed two rounds of resident blocks.  So it runs on the
   // small-multiexp stream (high priority, every CU), with its bucket reduction shaped for one round
-  // of the whole GPU.
-  static const bool last_full_env = [] {
-    const char* e = getenv("BH_LAST_TAIL_FULL");
-    return !(e && e[0] == '0');
-  }();
-  const bool last_full = last_full_env && !serial && !ctx->borrowed_streams && ctx->cu_masked;
+  // of the whole GPU (not on a pipelined batch lane, whose next proof's first accumulation would
+  // queue behind it).
+  const bool last_full = !serial && !ctx->borrowed_streams && ctx->cu_masked;
   hipEvent_t* jev = ctx->jev;  // [2j,2j+1] accumulate timing, [16+j] sorted, [24+j] accumulated,
                                // [32] start, [33] density maps ready
   BH_TRY_HIP(hipEventRecord(jev[32], sA));
@@ -935,7 +898,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   ShareGeom geom;
   if (dh) {
     geom.N = dh->N; geom.rank = dh->rank; geom.L = L; geom.M = dh->M; geom.C = dh->C;
-    if (ctx->stream4d && !serial) sH = ctx->stream4d;  // on half the CUs (bh_ctx_create)
   }
   const ShareGeom* sg = dh ? &geom : nullptr;
   const uint32_t* sh_buf = dh ? dh->hbuf.as<uint32_t>() : nullptr;
@@ -1042,8 +1004,8 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (jobs[j].table_c) n_large++;
     if (use_table[j]) n_table++;
   }
-  // ---- H (prover.rs:210-234), device resident.  Where it is enqueued depends on h_mode
-  // (below); only h's sort waits for it.
+  // ---- H (prover.rs:210-234), device resident.  Where it is enqueued: see 'H placement' below;
+  // only h's sort waits for it.
   auto enqueue_h = [&](hipEvent_t after) -> bh_status {
     if (up && up->on_vector) {
       // bh_prove: the uploading thread enqueues H on sH vector by vector, each behind its own
@@ -1097,13 +1059,9 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
            a.bk_hi == b.bk_hi;
   };
   // ... and one over a sparser density map (a_aux, b_aux under l's dense one) compacts it
-  static const bool derive_on = [] {  // BH_SORT_DERIVE=0: full sorts only (A/B experiments)
-    const char* e = getenv("BH_SORT_DERIVE");
-    return !(e && e[0] == '0');
-  }();
   auto derivable = [&](int i, int j) {
     const MsmShape &a = shapes[i], &b = shapes[j];
-    return derive_on && jobs[i].sc == jobs[j].sc && !jobs[i].idx && jobs[j].idx && !jobs[i].is_h && los[i] == los[j] &&
+    return jobs[i].sc == jobs[j].sc && !jobs[i].idx && jobs[j].idx && !jobs[i].is_h && los[i] == los[j] &&
            his[i] == his[j] && a.c == b.c && a.W == b.W && a.NB == b.NB && a.Wb == b.Wb && a.pre == b.pre &&
            a.bk_lo == b.bk_lo && a.bk_hi == b.bk_hi;
   };
@@ -1185,51 +1143,26 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     MsmTiming tm;
     tm.ev_acc_begin = acc_events_on() ? jev[2 * j] : nullptr;
     tm.ev_acc_end = acc_events_on() ? jev[2 * j + 1] : nullptr;
-    tm.ev_half = shapes[j].halves ? jev[36 + j] : nullptr;
     const uint32_t* bases = use_table[j] ? J.srs->win_global() : J.srs->pts.as<uint32_t>();
     if (J.g2) BH_TRY_HIP(msm_accumulate<G2Ops>(ctx->pw2[J.out], st, bases, n, shapes[j], &tm));
     else BH_TRY_HIP(msm_accumulate<G1Ops>(ctx->pw1[J.out], st, bases, n, shapes[j], &tm));
     BH_TRY_HIP(hipEventRecord(jev[24 + j], st));
     return BH_OK;
   };
-  // BH_TAIL_DEFER=1: every reduction tail starts after the LAST accumulation (A/B: tails
-  // running beside the accumulations take SIMD slots from them)
-  static const bool tail_defer = [] {
-    const char* e = getenv("BH_TAIL_DEFER");
-    return e && e[0] == '1';
-  }();
-  int last_acc = -1;
   auto tail_job = [&](int j, hipStream_t st) -> bh_status {
     const Job& J = jobs[j];
     const size_t n = his[j] - los[j];
-    // halves: from the lower half's end; msm_back waits for the rest before the upper half
-    BH_TRY_HIP(hipStreamWaitEvent(st, jev[(shapes[j].halves ? 36 : 24) + j], 0));
-    if (tail_defer && last_acc >= 0) BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + last_acc], 0));
+    BH_TRY_HIP(hipStreamWaitEvent(st, jev[24 + j], 0));
     // entries = mixed additions of this multiexp (offsets[nbt]), for the VALU roofline
     // (copied here, off the accumulation stream)
     const uint32_t* offs = J.g2 ? ctx->pw2[J.out].offsets : ctx->pw1[J.out].offsets;
     BH_TRY_HIP(hipMemcpyAsync(&ctx->host_counts[j], offs + (size_t)shapes[j].Wb * shapes[j].NB, 4,
                               hipMemcpyDeviceToHost, st));
-    // The longest bucket span picks the continuation fold.  Default: the tail kernels read the
-    // sort's span words on the device, so enqueueing a tail never waits for its sort (a pipelined
-    // batch hands the streams on to the next proof without waiting for this one's h sort, which
-    // follows H).  BH_TAIL_HOST_SPAN=1: the host reads it once the sort is done (round 2 scheme;
-    // it also skips k_cont_seq's launch when the spans are short).
-    static const bool host_span = [] {
-      const char* e = getenv("BH_TAIL_HOST_SPAN");
-      return e && e[0] == '1';
-    }();
-    int span = -1;
-    const uint32_t* dspan = nullptr;
-    if (n >= SMALL_JOB) {
-      if (host_span) {
-        BH_TRY_HIP(hipEventSynchronize(jev[16 + j]));
-        span = (int)max_span_host(ctx->host_spans + (size_t)j * MAX_SPAN_BLOCKS,
-                                  (size_t)shapes[j].Wb * shapes[j].red_nb());
-      } else {
-        dspan = ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS;
-      }
-    }
+    // The longest bucket span picks the continuation fold: the tail kernels read the sort's span
+    // words on the device, so enqueueing a tail never waits for its sort (a pipelined batch hands
+    // the streams on to the next proof without waiting for this one's h sort, which follows H)
+    const int span = -1;
+    const uint32_t* dspan = n >= SMALL_JOB ? ctx->dspan.as<uint32_t>() + (size_t)j * MAX_SPAN_BLOCKS : nullptr;
     if (J.g2)
       BH_TRY_HIP(msm_back<G2Ops>(ctx->pw2[J.out], st, n, shapes[j], ctx->host_out2 + 128 * J.out, span, jev[24 + j],
                                  dspan));
@@ -1261,72 +1194,30 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // the critical path: give its bucket reduction more, shorter chains (fewer buckets per
   // thread: 2L + 2 log2(BT) + log2(L) serial point operations in k_reduce_blocks), while
   // the earlier tails, which share the SIMDs with accumulations, keep the work-lean shape.
+  // (Tried and removed: the last multiexp accumulated and reduced as two bucket halves so the
+  // lower half's reduction runs beside the upper half's accumulation, +0.8 ms per 2^22 proof,
+  // profiles/r03_ab_last_halves.txt; fewer rounds for the last accumulation, within noise.)
   if (nbig > 0) {
     MsmShape& sl = shapes[big[nbig - 1]];
-    static const int last_threads_env = [] {
-      const char* e = getenv("BH_LAST_TAIL_THREADS");
-      return e ? atoi(e) : 0;
-    }();
-    // default: one round of resident k_reduce_blocks blocks on the CUs the last tail runs on
-    const int last_threads = last_threads_env ? last_threads_env
-                             : last_full       ? (int)std::min<size_t>(reduce_resident_threads(ctx, true), 1 << 20)
-                                               : 65536;
-    // BH_LAST_HALVES=1: with one shared bucket window, the last multiexp is accumulated as two
-    // bucket halves and the lower half's reduction (work-lean L) runs beside the upper half's
-    // accumulation: only the upper half's, with the short chains, is left at the end.  Parity
-    // green, but +0.8 ms per 2^22 proof (60.79 against 60.00 ms, profiles/r03_ab_last_halves.txt):
-    // the lower half's latency-bound reduction slows the upper accumulation by more than the
-    // shorter tail saves.  Off by default.
-    static const bool last_halves = [] {
-      const char* e = getenv("BH_LAST_HALVES");
-      return e && e[0] == '1';
-    }();
-    const bool halves = last_halves && sl.Wb == 1 && sl.NB >= 4096 && !serial && !sl.bucket_shard();
-    if (last_threads > 0) {
-      const int nb = halves ? sl.NB / 2 : (int)sl.red_nb();
-      int L = sl.L;
-      while (L > 1 && (size_t)sl.Wb * (size_t)(nb / L) < (size_t)last_threads) L >>= 1;
-      if (halves) {
-        sl.halves = 1;
-        sl.L2 = L;
-      } else {
-        sl.L = L;
-      }
-    } else if (halves) {
-      sl.halves = 1;
-      sl.L2 = sl.L;
-    }
-    // BH_LAST_ACC_ROUNDS = r (A/B experiments): the last accumulation in r resident rounds instead
-    // of fit_segments' 3 (longer segments: fewer continuation partials for its tail to fold)
-    static const int last_rounds = [] {
-      const char* e = getenv("BH_LAST_ACC_ROUNDS");
-      return e ? atoi(e) : 0;
-    }();
-    if (last_rounds > 0 && last_rounds < 3) sl.S = std::min(sl.S * 3 / last_rounds, 1 << 16);
+    // one round of resident k_reduce_blocks blocks on the CUs the last tail runs on
+    const int last_threads =
+        last_full ? (int)std::min<size_t>(reduce_resident_threads(ctx, true), 1 << 20) : 65536;
+    const int nb = (int)sl.red_nb();
+    int L = sl.L;
+    while (L > 1 && (size_t)sl.Wb * (size_t)(nb / L) < (size_t)last_threads) L >>= 1;
+    sl.L = L;
   }
-  // H placement (BH_H_MODE): 0 = first, alone, the accumulations waiting for it;
-  // 1 = from the start, concurrent with everything (the default); 2 = after the first
-  // accumulation (round 3's replicated default, when the first accumulation -- b_g2_aux --
-  // took a SIMD's whole register file and H's passes could not share its SIMDs).  Since the G2
-  // accumulation keeps ZZ/ZZZ in LDS (268 registers, msm_impl.cuh accumulate_lds), H's NTT passes
-  // co-reside with it: same-box A/B at 2^22, 55.1-55.3 ms per proof with 1 against 57.4-58.2 with
-  // 2 (3: 55.7-56.2; profiles/r04_ab_hmode_g2.txt).
-  static const int h_mode_env = [] {
-    const char* e = getenv("BH_H_MODE");
-    return e ? atoi(e) : -1;
-  }();
-  // 3 = concurrent with everything like 1, but enqueued by the host after the first
-  // accumulation's launch; 4 = between the first sorts and the first accumulation.  Round 3,
-  // distributed H on its masked half of the CUs, at N = 8 in the one-GPU rehearsal: 1 (default)
-  // 10.26-10.36 ms per rank, 2 10.27, 3 10.37-10.42, 4 10.39, and 1 enqueued by a helper host
-  // thread 10.44, and H held until the first sorts are done 10.61-10.73 against 10.28-10.37 (neither
-  // kept) -- profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt.
-  // 5 = enqueued right before h's own sort and accumulation, after every other sort and
-  // accumulation: the default from host buffers (bh_prove), where enqueue_h first waits on the host
-  // until a, b, c are staged -- placed first (mode 1) that wait held back every other enqueue (68.4
-  // against 56.5 ms resident); placed last, the device is busy with the queued accumulations
-  // meanwhile, and H still starts as soon as its upload lands, beside the first accumulation.
-  int h_mode = h_mode_env >= 0 ? h_mode_env : (up ? 5 : 1);
+  // H placement.  A resident witness enqueues H first, running beside everything: since the G2
+  // accumulation keeps ZZ/ZZZ in LDS (268 registers, msm_impl.cuh accumulate_lds) H's NTT passes
+  // co-reside with it (same-box A/B at 2^22: 55.1-55.3 ms per proof against 57.4-58.2 with H after
+  // the first accumulation, profiles/r04_ab_hmode_g2.txt).  Other placements were measured and
+  // removed: H enqueued after the first accumulation's launch, between the first sorts and the first
+  // accumulation, from a helper host thread, or held on the device until the first sort is done
+  // (N = 8 rehearsal within 0.1 ms or slower, profiles/r03_ab_hmode_N8.txt, r03_ab_hmode_more_N8.txt,
+  // r05_ab_sched_knobs_N1_2_8.txt).  From host buffers (bh_prove) the uploading thread enqueues H
+  // vector by vector behind each upload (on_vector); here only h's own sort and accumulation wait on
+  // the host for that enqueue, so they are enqueued last.
+  bool h_late = up != nullptr;
   // the small multiexps run whole on their own stream, after the density maps
   BH_TRY_HIP(hipStreamWaitEvent(sT, jev[33], 0));
   auto run_small = [&]() -> bh_status {
@@ -1364,58 +1255,33 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if (sorder[r] == big[0] || (nbig > 1 && h_pos != 1 && sorder[r] == big[1])) pre_sorts = r + 1;
   bool h_in_pre = false;
   for (int r = 0; r < pre_sorts; r++) h_in_pre = h_in_pre || jobs[sorder[r]].is_h;
-  if (h_in_pre && (h_mode >= 2)) h_mode = 1;  // h's own sort is among the first: H first
-  if (h_mode == 0 || h_mode == 1) {
-    if ((s = enqueue_h(jev[33]))) return s;
-  }
+  if (h_in_pre) h_late = false;  // h's own sort is among the first: H first
+  if (!h_late && (s = enqueue_h(jev[33]))) return s;
 
   for (int r = 0; r < pre_sorts; r++) {
     if ((s = sort_h_or(sorder[r]))) return s;
   }
-  if (h_mode == 0) BH_TRY_HIP(hipStreamWaitEvent(sA, ctx->ev[1], 0));
-  // 4 = enqueued between the first sorts and the first accumulation: the sorts are not held up
-  // by the host's ~0.4 ms of H enqueueing (mode 1), and H's first kernels reach the device
-  // before the first accumulation fills every CU (mode 3)
-  if (h_mode == 4 && (s = enqueue_h(jev[33]))) return s;
-  // 6 = enqueued there too, but starting on the device only once the first real sort is done:
-  // H's NTT passes fill every SIMD's register file (4 waves x 128 VGPRs) and LDS, so beside them
-  // the first sort's workgroups only got slots when H reached its first exchange (round-5 traces:
-  // the first k_part_count started 0.4 ms (N = 8) and 1.27 ms (N = 2) after the density maps)
-  if (h_mode == 6) {
-    int first_sort = -1;
-    for (int r = 0; r < pre_sorts && first_sort < 0; r++)
-      if (sorted_from[sorder[r]] == sorder[r]) first_sort = sorder[r];
-    if ((s = enqueue_h(first_sort >= 0 ? jev[16 + first_sort] : jev[33]))) return s;
-  }
-  static const bool first_own = [] {
-    const char* e = getenv("BH_FIRST_ACC_STREAM");
-    return !(e && e[0] == '0');
-  }();
+  // The first accumulation (G2: 268 registers, one wave per SIMD) runs on the small-multiexp
+  // stream (idle when the public-input multiexps are on the host), so the G1 accumulations start
+  // beside it instead of after it: same-box A/B at 2^22 54.66-55.17 against 55.01-55.45 ms
+  // (profiles/r04_ab_first_acc_stream.txt).
+  const bool first_own = nsmall == 0 && !serial;
   if (nbig > 0) {
     // wait for the last pre-sort that is a real sort: a trailing copy of another multiexp's
     // entries (b_g1_aux from b_g2_aux) is ~0.15 ms of blits that can run beside the accumulation
     int wait_j = big[0];
     for (int r = 0; r < pre_sorts; r++)
       if (sorted_from[sorder[r]] == sorder[r]) wait_j = sorder[r];
-    // The first accumulation (G2: 268 registers, one wave per SIMD) runs on the small-multiexp
-    // stream (idle when the public-input multiexps are on the host), so the G1 accumulations start
-    // beside it instead of after it: same-box A/B at 2^22 54.66-55.17 against 55.01-55.45 ms
-    // (profiles/r04_ab_first_acc_stream.txt).  BH_FIRST_ACC_STREAM=0: on the main stream.
-    hipStream_t s0 = (first_own && nsmall == 0 && !serial) ? sT : sA;
+    hipStream_t s0 = first_own ? sT : sA;
     BH_TRY_HIP(hipStreamWaitEvent(s0, jev[16 + wait_j], 0));
     if ((s = acc_job(big[0], s0))) return s;
   }
   // With the first accumulation on its own stream, the second one (G1: b_g1_aux, whose sorted
   // entries are a copy among the first sorts) is enqueued right behind it, before the remaining
-  // sorts and H: those are ~20-40 host enqueues (~0.7 ms per rank at N = 8 in the round-5 kernel
+  // sorts: those are ~20-40 host enqueues (~0.7 ms per rank at N = 8 in the round-5 kernel
   // trace, 1.6 ms at N = 2), during which the G2 accumulation ran alone on its one wave per SIMD.
-  // BH_G1_EARLY=0: after the remaining sorts (round 4).
-  static const bool g1_early = [] {
-    const char* e = getenv("BH_G1_EARLY");
-    return !(e && e[0] == '0');
-  }();
   int q_first = 1;
-  if (g1_early && nbig > 1 && !jobs[big[1]].is_h && !serial && first_own && nsmall == 0) {
+  if (nbig > 1 && !jobs[big[1]].is_h && first_own) {
     bool pre = false;  // its sort is among the pre-sorts (enqueued above)
     for (int r = 0; r < pre_sorts; r++) pre = pre || sorder[r] == big[1];
     if (pre) {
@@ -1424,28 +1290,20 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     }
   }
   const auto t_acc0 = std::chrono::steady_clock::now();
-  if (h_mode == 2 && (s = enqueue_h(nbig > 0 ? jev[24 + big[0]] : jev[33]))) return s;
-  if (h_mode == 3 && (s = enqueue_h(jev[33]))) return s;
   const auto t_h = std::chrono::steady_clock::now();
-  const bool h_late = h_mode == 5;
   for (int r = pre_sorts; r < ns; r++) {
     if (h_late && jobs[sorder[r]].is_h) continue;  // behind H, enqueued below
     if ((s = sort_h_or(sorder[r]))) return s;
   }
   const auto t_sorts = std::chrono::steady_clock::now();
-  // Two accumulation lanes (default; BH_ACC_LANES=1: every accumulation after the first on the main
-  // stream): the accumulations after the first two go to whichever of the two accumulation streams
+  // Two accumulation lanes: the accumulations after the first two go to whichever of the two accumulation streams
   // (the first one's, the main one) has less queued work (mixed additions, a G2 one weighted 2.75x).
   // Consecutive accumulations on one stream are separated by a barrier (the next kernel dispatches
   // only once the last block of the previous one is done), and in that moment other streams'
   // pending kernels take the freed slots (round-5 drop-in trace: 1.4 and 2.9 ms of main-stream idle
   // before a_aux and h).  Rehearsal N = 8 9.85-9.92 against 10.05-10.23 ms per rank, N = 1 and the
   // bench within noise (profiles/r05_ab_acc_lanes.txt).
-  static const int acc_lanes = [] {
-    const char* e = getenv("BH_ACC_LANES");
-    return e ? atoi(e) : 2;
-  }();
-  const bool two_lanes = acc_lanes == 2 && first_own && nsmall == 0 && !serial && !ctx->borrowed_streams && nbig > 2;
+  const bool two_lanes = first_own && !ctx->borrowed_streams && nbig > 2;
   auto acc_cost = [&](int j) {
     const double e = (double)jobs[j].used * (double)(shapes[j].W ? shapes[j].W : 1);
     return jobs[j].g2 ? 2.75 * e : e;
@@ -1468,7 +1326,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if ((s = acc_job(big[q], sq))) return s;
   }
   if (!h_done && (s = enqueue_h(jev[33]))) return s;  // (no large h job: H still runs)
-  if (nbig > 0) last_acc = big[nbig - 1];
   if ((s = run_small())) return s;
   // The host waits below are on events of THIS proof's work (not stream syncs): on a pipelined
   // batch lane the streams soon hold the next proof's work behind it.
@@ -1484,17 +1341,6 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (t_lane.after_accs) t_lane.after_accs();
   if (t_lane.before_tails) t_lane.before_tails();
   if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = sT;
-  // BH_G2_TAIL_FULL=1 (A/B): the G2 multiexps' reduction tails on the witness-copy stream (every CU,
-  // high priority; a resident proof never copies on it, bh_prove's uploads are done long before)
-  // instead of a quarter-CU tail stream: at N = 8 the G2 tail (continuation fold 3.7 ms, reduction
-  // 2.3 ms on 64 CUs) ends the rank's proof (gpurun_out/r5rt trace)
-  static const bool g2_tail_full = [] {
-    const char* e = getenv("BH_G2_TAIL_FULL");
-    return e && e[0] == '1';
-  }();
-  if (g2_tail_full && !serial && !ctx->borrowed_streams)
-    for (int q = 0; q + 1 < nbig; q++)
-      if (jobs[big[q]].g2) tails[q] = ctx->h2d;
   for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
     BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
@@ -1967,15 +1813,8 @@ bh_status bh_rehearse_rank(bh_ctx* ctx, const bh_params* params, const bh_witnes
   return BH_OK;
 }
 
-// default pipelined lanes of bh_prove_batch (BH_BATCH_LANES: A/B experiments)
-static int batch_lanes() {
-  static const int v = [] {
-    const char* e = getenv("BH_BATCH_LANES");
-    const int x = e ? atoi(e) : 2;
-    return (x >= 1 && x <= 16) ? x : 2;
-  }();
-  return v;
-}
+// default pipelined lanes of bh_prove_batch: two (a third adds nothing, profiles/r04_ab_c5_lanes.txt)
+static int batch_lanes() { return 2; }
 
 bh_status bh_prove_batch(bh_ctx* ctx, const bh_params* params, const bh_witness* const* ws, size_t k,
                          const uint64_t r_in[4], const uint64_t s_in[4], int lanes, uint8_t* proofs_out) {
@@ -2206,12 +2045,9 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
   // H from the uploading thread: each of a, b, c is converted and transformed on the H stream
   // as soon as its own upload has landed (stream order behind vec[v]), so H starts ~1/3 of the
   // a, b, c upload after aux and runs beside the first accumulations, and no host thread that
-  // enqueues the multiexps ever waits for the upload of a, b, c (prover.rs:210-231).
-  // BH_PROVE_H_UPLOADER=0: H enqueued by compute_msms after the whole upload (round-4 scheme).
-  static const bool h_uploader = [] {
-    const char* e = getenv("BH_PROVE_H_UPLOADER");
-    return !(e && e[0] == '0') && !prover_serial();
-  }();
+  // enqueues the multiexps ever waits for the upload of a, b, c (prover.rs:210-231).  (One stream,
+  // BH_PROVER_SERIAL: compute_msms enqueues H after the whole upload.)
+  const bool h_uploader = !prover_serial();
   Domain* D = nullptr;
   if (h_uploader) {
     // everything the H stages touch, allocated before the uploading thread can enqueue them
@@ -2224,21 +2060,13 @@ bh_status bh_prove(bh_ctx* ctx, const bh_params* params, const uint64_t* a, cons
       uint32_t* abc = ctx->staging.as<uint32_t>();
       BH_TRY_HIP(hipStreamWaitEvent(sH, up.vec[v], 0));
       if (v == 0) BH_TRY_HIP(hipEventRecord(ctx->ev[0], sH));
-      bh_status hs;
-      if (h_fused_convert()) {
-        // the ifft's first pass reads the uploaded bls12_381-Montgomery words in place (their
-        // radix folded into its scale, run_h_vector); only the padding is written first
-        uint32_t* raw = const_cast<uint32_t*>(w->abc.as<uint32_t>());
-        if (m > nc) BH_TRY_HIP(hipMemsetAsync(raw + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
-        hs = run_h_vector(ctx, D, abc, sH, raw, v, true);
-      } else {
-        // bls12_381 Montgomery -> device Montgomery into the H block's buffer, zero padding
-        if (nc) launch_fr_convert(w->abc.as<uint32_t>() + (size_t)v * m * 8, abc + (size_t)v * m * 8, nc,
-                                  fr_to_dev_const(), 0, sH);
-        if (m > nc) BH_TRY_HIP(hipMemsetAsync(abc + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
-        BH_TRY_HIP(hipGetLastError());
-        hs = run_h_vector(ctx, D, abc, sH, nullptr, v);
-      }
+      // the ifft's first pass reads the uploaded bls12_381-Montgomery words in place (their radix
+      // folded into its scale, run_h_vector); only the padding is written first.  (A conversion
+      // kernel first, round 5's first scheme, waited for slots beside the accumulations: 9.5 ms
+      // for a trivial kernel in the round-5 drop-in trace.)
+      uint32_t* raw = const_cast<uint32_t*>(w->abc.as<uint32_t>());
+      if (m > nc) BH_TRY_HIP(hipMemsetAsync(raw + ((size_t)v * m + nc) * 8, 0, (m - nc) * 32, sH));
+      bh_status hs = run_h_vector(ctx, D, abc, sH, raw, v, true);
       if (hs) return hs;
       if (v == 2) {
         // the last pass writes h as canonical scalars, natural order, truncated to m-1 (prover.rs:227-231)

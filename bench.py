@@ -206,7 +206,7 @@ def c5_leg(bh, args, ctx, world, rank, comm, r, s, barrier):
                         f"(distinct preimages), {len(mine)} per GPU, bh_prove_batch",
             "value": round(args.c5 * n_c / el, 1), "unit": "constraints/s", "proofs": args.c5,
             "ms_per_proof": round(el * 1e3 / max(1, len(mine)), 3), "batch_s": round(el, 3),
-            "lanes": args.c5_lanes or int(os.environ.get("BH_BATCH_LANES", "2")), "proofs_match_single": ok, "synthesis_s": round(t_syn, 2)}
+            "lanes": args.c5_lanes or 2, "proofs_match_single": ok, "synthesis_s": round(t_syn, 2)}
 
 
 def domain_leg(bh, ctx, asg, n_constraints, reps=2):

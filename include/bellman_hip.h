@@ -13,6 +13,8 @@
  *   bh_mul_assign / bh_sub_assign
  *                          EvaluationDomain methods      domain.rs:81-189
  *   bh_domain_size         EvaluationDomain::from_coeffs  domain.rs:47-79
+ *   bh_evdom_*             EvaluationDomain with its coefficients resident in HBM
+ *                                                         domain.rs:21-190
  *   bh_compute_h           the H block of create_proof   groth16/prover.rs:210-231
  *   bh_params_*            Parameters / ParameterSource  groth16/mod.rs:224-477
  *   bh_prove / bh_prove_witness
@@ -20,7 +22,9 @@
  *
  * Conventions
  *   - Plain pointers and sizes only; the caller owns every host buffer and the
- *     library never retains a caller pointer after a call returns.
+ *     library never retains a caller pointer after a call returns -- except the inputs of
+ *     bh_compute_h_scalars and bh_evdom_from_coeffs / bh_evdom_write, read asynchronously
+ *     until the sync named there.
  *   - Fr vectors ("Montgomery") use the bls12_381 0.6 in-memory layout:
  *     4 little-endian u64 limbs of x * 2^256 mod r per element.
  *   - Exponents for bh_multiexp are Scalar::to_le_bits() words (canonical,
@@ -304,7 +308,7 @@ bh_status bh_comm_allreduce_max(bh_comm* c, double* inout);
 /* what RCCL reports for the communicator: out = {rank count, this rank, HIP device id} */
 bh_status bh_comm_info(const bh_comm* c, int out[3]);
 /* This rank's partial record (rank/nranks from the communicator).  For nranks a power of two
- * in [BH_DIST_H_MIN (default 4), 16] and m >= 2*nranks^2 the H block is distributed instead
+ * in [2, 16] and m >= 2*nranks^2 the H block is distributed instead
  * of replicated: every NTT is a local m/nranks-point NTT plus one ncclSend/ncclRecv
  * all-to-all, three all-to-alls per proof, and this rank's h multiexp covers exactly the h
  * coefficients it ends with (a strided set, not the range of bh_shard_range).  Otherwise

@@ -1079,3 +1079,21 @@ def test_proof_stats_accumulation_wall_time(ctx):
     g1_sum, g2_sum, g1_wall, g2_wall = st[2], st[5], st[21], st[22]
     assert 0 < g1_wall <= g1_sum * 1.0001 and 0 < g2_wall <= g2_sum * 1.0001
     assert 0 < st[8] <= 32 * st[4] and 0 < st[9] <= 32 * st[7]
+
+
+@pytest.mark.parametrize("env", [{"BH_PROVER_SERIAL": "1"}, {"BH_ACC_EVENTS": "0"}])
+def test_diagnostic_modes_give_the_same_proof(ctx, monkeypatch, env):
+    """The library's two diagnostic switches, read per proof: BH_PROVER_SERIAL=1 (every kernel on
+    one stream, for per-kernel profiles; bh_prove then enqueues H after the whole upload) and
+    BH_ACC_EVENTS=0 (no timing events around the accumulations) give the default proof, from a
+    resident witness and from host buffers."""
+    bh = _bh()
+    rounds = (1 << 15) - 1
+    params = bh.Parameters.chain(ctx, rounds)
+    w = bh.Witness.chain(ctx, rounds)
+    asg = bh.chain_assignment(rounds)
+    want = bh.prove_witness(ctx, params, w, 27134, 17146)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert bh.prove_witness(ctx, params, w, 27134, 17146) == want
+    assert bh.prove(ctx, params, asg, 27134, 17146) == want

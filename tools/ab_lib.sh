@@ -21,7 +21,9 @@ import json, sys
 for l in open(sys.argv[2]):
     if l.startswith("{"):
         d = json.loads(l)
-        print(sys.argv[1], d["ms_per_step"], json.dumps(d["breakdown_ms"]))
+        dr = d.get("dropin") or {}
+        print(sys.argv[1], d["ms_per_step"], "dropin", dr.get("ms_per_step"),
+              "landed", (dr.get("landed_ms") or {}).get("per_call", [None])[-1], json.dumps(d["breakdown_ms"]))
 EOF
     tail -1 $O/summary.txt
   done
