@@ -481,7 +481,7 @@ bh_status upload_split_table(bh_ctx* ctx, DevBuf& lo, DevBuf& hi, const Fr& g, c
 }
 
 void ctx_sync_all(bh_ctx* ctx) {
-  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->bg.cst,
+  for (hipStream_t st : {ctx->h2d, ctx->stream, ctx->stream2, ctx->stream3, ctx->stream4, ctx->stream5, ctx->bg.cst,
                          ctx->bg.st})
     if (st) (void)hipStreamSynchronize(st);
   for (hipStream_t st : ctx->tstream)
@@ -785,7 +785,8 @@ bh_status bh_ctx_create(int device, bh_ctx** out) {
   }
   if (hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, side) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, side) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->stream4, hipStreamNonBlocking, side) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream5, hipStreamNonBlocking, side) != hipSuccess) {
     release_mask(c); delete c;
     return BH_ERR_HIP;
   }
@@ -847,6 +848,7 @@ __attribute__((visibility("hidden"))) bh_status ctx_create_lane(bh_ctx* primary,
   c->stream2 = primary->stream2;
   c->stream3 = primary->stream3;
   c->stream4 = primary->stream4;
+  c->stream5 = primary->stream5;
   c->h2d = primary->h2d;
   for (int q = 0; q < bh_ctx::TAIL_STREAMS; q++) c->tstream[q] = primary->tstream[q];
   c->tables = primary->tables;
@@ -919,6 +921,7 @@ bh_status bh_ctx_destroy(bh_ctx* ctx) {
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream3);
     (void)hipStreamDestroy(ctx->stream4);
+    if (ctx->stream5) (void)hipStreamDestroy(ctx->stream5);
     for (auto& t : ctx->tstream) (void)hipStreamDestroy(t);
   }
   const int dev = ctx->device;

@@ -263,6 +263,7 @@ struct bh_ctx {
   hipStream_t stream2 = nullptr;  // prover: the multiexps' reduction tails (high priority)
   hipStream_t stream3 = nullptr;  // prover: density maps and the multiexps' sorts (high priority)
   hipStream_t stream4 = nullptr;  // prover: H pipeline
+  hipStream_t stream5 = nullptr;  // prover: the second G1 accumulation lane
   // prover: reduction-tail streams (high priority, CU-masked on the first context of a device).
   // A proof has at most 5 large multiexps unless the public inputs number in the thousands;
   // more tails share these round robin.  Kept small for the device's hardware-queue budget

@@ -1296,19 +1296,23 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     if ((s = sort_h_or(sorder[r]))) return s;
   }
   const auto t_sorts = std::chrono::steady_clock::now();
-  // Two accumulation lanes: the accumulations after the first two go to whichever of the two accumulation streams
-  // (the first one's, the main one) has less queued work (mixed additions, a G2 one weighted 2.75x).
-  // Consecutive accumulations on one stream are separated by a barrier (the next kernel dispatches
-  // only once the last block of the previous one is done), and in that moment other streams'
-  // pending kernels take the freed slots (round-5 drop-in trace: 1.4 and 2.9 ms of main-stream idle
-  // before a_aux and h).  Rehearsal N = 8 9.85-9.92 against 10.05-10.23 ms per rank, N = 1 and the
-  // bench within noise (profiles/r05_ab_acc_lanes.txt).
+  // Accumulation lanes: the accumulations after the first two go to whichever of three accumulation
+  // streams (the first one's, the main one, stream5) has the least queued work (mixed additions, a G2
+  // one weighted 2.75x).  Consecutive accumulations on one stream are separated by a barrier (the
+  // next kernel dispatches only once the last block of the previous one is done: ~0.12 ms between
+  // them in the round-5 traces), and in that moment other streams' pending kernels take the freed
+  // slots (round-5 drop-in trace: 1.4 and 2.9 ms of main-stream idle before a_aux and h).  Two lanes
+  // (round 5): rehearsal N = 8 9.85-9.92 against 10.05-10.23 ms per rank (profiles/r05_ab_acc_lanes.txt);
+  // with the G2 accumulation holding one lane for most of the proof, the G1 ones still ran back to
+  // back on the other, so round 6 adds a third: the 2^22 bench 54.4-54.6 against 54.8-55.0 ms, bh_prove
+  // 58.7-58.9 against 59.5-59.7, N = 2 30.4 against 30.8-31.2 ms per rank, N = 1 and 8 within noise
+  // (profiles/r06_ab_acc_lanes3.txt).
   const bool two_lanes = first_own && !ctx->borrowed_streams && nbig > 2;
   auto acc_cost = [&](int j) {
     const double e = (double)jobs[j].used * (double)(shapes[j].W ? shapes[j].W : 1);
     return jobs[j].g2 ? 2.75 * e : e;
   };
-  double lane_load[2] = {nbig > 0 ? acc_cost(big[0]) : 0.0, 0.0};  // [0] sT, [1] sA
+  double lane_load[3] = {nbig > 0 ? acc_cost(big[0]) : 0.0, 0.0, 0.0};  // [0] sT, [1] sA, [2] stream5
   for (int q = 1; q < q_first; q++) lane_load[1] += acc_cost(big[q]);
   bool h_done = !h_late;
   for (int q = q_first; q < nbig; q++) {
@@ -1319,9 +1323,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     }
     hipStream_t sq = sA;
     if (two_lanes) {
-      const int l = lane_load[0] < lane_load[1] ? 0 : 1;
+      int l = lane_load[0] < lane_load[1] ? 0 : 1;
+      if (lane_load[2] < lane_load[l]) l = 2;
       lane_load[l] += acc_cost(big[q]);
-      sq = l == 0 ? sT : sA;
+      sq = l == 0 ? sT : l == 1 ? sA : ctx->stream5;
     }
     if ((s = acc_job(big[q], sq))) return s;
   }
