@@ -243,11 +243,14 @@ size_t density_set(const uint64_t* density_words, size_t n) {
 // goes back and the job is left without one.
 // G2 jobs accumulate on the small-multiexp stream (stream2, idle under the seam), so a G2
 // accumulation runs beside the G1 ones as bh_prove's first accumulation does, instead of queueing
-// behind them on the main stream (create_proof submits b_g2_aux last: prover.rs:298-307).
+// behind them on the main stream (create_proof submits b_g2_aux last: prover.rs:298-307).  G1 jobs
+// alternate between the main stream and stream5, as bh_prove's accumulation lanes do, so
+// consecutive G1 accumulations do not wait at a stream barrier for each other's last blocks.
 JobStreams job_streams(bh_ctx* ctx, bool g2) {
-  static std::atomic<unsigned> rr{0};
-  return JobStreams{ctx->stream3, g2 ? ctx->stream2 : ctx->stream,
-                    ctx->tstream[rr.fetch_add(1) % bh_ctx::TAIL_STREAMS]};
+  static std::atomic<unsigned> rr{0}, lane{0};
+  hipStream_t acc = ctx->stream2;
+  if (!g2) acc = (ctx->stream5 && (lane.fetch_add(1) & 1)) ? ctx->stream5 : ctx->stream;
+  return JobStreams{ctx->stream3, acc, ctx->tstream[rr.fetch_add(1) % bh_ctx::TAIL_STREAMS]};
 }
 
 // the slot back after a failed enqueue: whatever was enqueued for it has drained first
@@ -256,6 +259,7 @@ void fail_slot(bh_ctx* ctx, bh_job* job) {
   (void)hipStreamSynchronize(ctx->stream3);
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->stream2);
+  if (ctx->stream5) (void)hipStreamSynchronize(ctx->stream5);
   for (hipStream_t t : ctx->tstream) (void)hipStreamSynchronize(t);
   give_slot(*job->reg, job->slot);
   job->slot = nullptr;

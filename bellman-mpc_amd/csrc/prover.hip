@@ -1307,7 +1307,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // back on the other, so round 6 adds a third: the 2^22 bench 54.4-54.6 against 54.8-55.0 ms, bh_prove
   // 58.7-58.9 against 59.5-59.7, N = 2 30.4 against 30.8-31.2 ms per rank, N = 1 and 8 within noise
   // (profiles/r06_ab_acc_lanes3.txt).
-  const bool two_lanes = first_own && !ctx->borrowed_streams && nbig > 2;
+  const bool multi_lane = first_own && !ctx->borrowed_streams && nbig > 2;
   auto acc_cost = [&](int j) {
     const double e = (double)jobs[j].used * (double)(shapes[j].W ? shapes[j].W : 1);
     return jobs[j].g2 ? 2.75 * e : e;
@@ -1322,7 +1322,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       h_done = true;
     }
     hipStream_t sq = sA;
-    if (two_lanes) {
+    if (multi_lane) {
       int l = lane_load[0] < lane_load[1] ? 0 : 1;
       if (lane_load[2] < lane_load[l]) l = 2;
       lane_load[l] += acc_cost(big[q]);
