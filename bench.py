@@ -30,12 +30,12 @@ sys.path.insert(0, os.path.join(ROOT, "bellman-mpc_amd"))
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 G1_PAIR_BYTES = 128       # 96 B affine base + 32 B scalar per (point, scalar)
 G2_PAIR_BYTES = 224
-TRAFFIC_FILE = "r05_final3_pmc_traffic_accumulate_g1.json"  # tools/pmc_round.py output for the 2^22 workload
+TRAFFIC_FILE = "r06_final_pmc_traffic_accumulate_g1.json"  # tools/pmc_round.py output for the 2^22 workload
 G1_MADD_PEAK = 7.04            # G mixed-add/s, tools/microbench/curvebench.hip on MI355X (profiles/r01_curvebench.txt)
 G1_MADD_PEAK_CLOCK_GHZ = 2.27  # the clock curvebench's G1 (2 waves) kernel held (profiles/r03_curvebench_clock.txt)
 MADS_PER_G1_MADD = 6 * 391 + 587 + 2 * 300  # 6 Fp-mul, Y3 as one two-product fe_mul2, 2 Fp-sqr
 MAD_U64_PEAK_TPS = 27.22       # T v_mad_u64_u32/s, tools/microbench/madbench.hip on MI355X
-PMC_FILE = "r05_final3_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_round.py over the 2^22 bench (+ held clocks, trace)
+PMC_FILE = "r06_final_pmc_2p22.json"  # tools/gpu_pmc.sh -> tools/pmc_round.py over the 2^22 bench (+ held clocks, trace)
 SOLO_WAVE_INSTR_RATE = 510.0   # G wave-instr/s: the G1 accumulation alone (6.38 G madd/s x 5116 lane-instr / 64;
                                # profiles/r03_ab_accumulate_variants.txt serial run, r03_pmc_2p22.json)
 
