@@ -1346,6 +1346,16 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   if (t_lane.after_accs) t_lane.after_accs();
   if (t_lane.before_tails) t_lane.before_tails();
   if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = sT;
+  // The G2 multiexp's reduction tail (continuation fold + reduction of G2 buckets, each addition
+  // ~3x a G1 one) on the first accumulation's stream, every CU, right behind the G2 accumulation,
+  // rather than on a quarter-CU tail stream: with three accumulation lanes the G1 accumulations end
+  // earlier and at N = 8 that latency-bound tail (2.9 + 1.6 + 0.8 ms on 64 CUs) became the rank's
+  // critical path (gpurun_out/r6l trace).  Same-box A/B: the 2^22 bench 53.9-54.0 against 54.3-54.8
+  // ms, bh_prove 57.9-58.2 against 58.4-58.9, rehearsal N = 1 / 2 / 8 at or below the base
+  // (profiles/r06_ab_g2_tail.txt).  (On a pipelined batch lane the streams are shared: tail streams.)
+  if (!serial && !ctx->borrowed_streams)
+    for (int q = 0; q + 1 < nbig; q++)
+      if (jobs[big[q]].g2) tails[q] = sT;
   for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
     BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
