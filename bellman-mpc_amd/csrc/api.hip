@@ -521,12 +521,20 @@ bh_status ctx_domain(bh_ctx* ctx, int L, Domain** out) {
   d->lo_bits = (L + 1) / 2;
   bh_status s;
   if ((s = upload_split_table(ctx, d->coset_lo, d->coset_hi, g, d->minv, L, d->lo_bits))) return s;
-  {
-    DevBuf lo32;  // (identical to coset_lo)
-    if ((s = upload_split_table(ctx, lo32, d->coset_hi32, g, mul(d->minv, fr_small(32)), L, d->lo_bits))) return s;
-  }
   if ((s = upload_split_table(ctx, d->icoset_lo, d->icoset_hi, ginv, d->minv, L, d->lo_bits))) return s;
   if ((s = upload_split_table(ctx, d->gpow_lo, d->gpow_hi, g, Fr::one(), L, d->lo_bits))) return s;
+  {
+    DevBuf lo32;
+    if ((s = upload_split_table(ctx, lo32, d->coset_hi32, g, mul(d->minv, fr_small(32)), L, d->lo_bits))) return s;
+    const DevBuf* src[3][2] = {{&d->coset_lo, &d->coset_hi}, {&lo32, &d->coset_hi32}, {&d->icoset_lo, &d->icoset_hi}};
+    DevBuf* dst[3] = {&d->coset_full, &d->coset32_full, &d->icoset_full};
+    for (int t = 0; t < 3; t++) {
+      BH_TRY_HIP(dst[t]->alloc(m * 36));
+      launch_expand_table(dst[t]->as<uint32_t>(), m, src[t][0]->as<uint32_t>(), src[t][1]->as<uint32_t>(), d->lo_bits,
+                          ctx->stream);
+    }
+    BH_TRY_HIP(hipStreamSynchronize(ctx->stream));
+  }
   uint32_t cst[3 * 9];
   fr_to_dev_limbs(d->minv, cst);
   fr_to_dev_limbs(d->zinv, cst + 9);
@@ -645,9 +653,8 @@ bh_status run_h_vector(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, 
   // then fft (DIT, bit-reversed -> natural) = coset_fft; c's storing pass computes
   // (a*b - c) / Z(g) into a (prover.rs:221-225: mul_assign, sub_assign, divide_by_z_on_coset)
   uint32_t* x = d_abc + (size_t)v * m * 8;
-  launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), D->coset_lo.as<uint32_t>(),
-             (raw_src ? D->coset_hi32 : D->coset_hi).as<uint32_t>(), D->lo_bits, st,
-             src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
+  launch_ntt(x, L, true, D->lv_inv.as<uint32_t>(), nullptr, (raw_src ? D->coset32_full : D->coset_full).as<uint32_t>(),
+             POW_FULL_TABLE, st, src_abc ? src_abc + (size_t)v * m * 8 : nullptr);
   NttEpilogue e;
   if (v == 2) {
     e.kind = NttEpilogue::AB_MINUS_C;
@@ -670,8 +677,8 @@ bh_status run_h_final(bh_ctx* ctx, Domain* D, uint32_t* d_abc, hipStream_t st, u
     e.out = hout;
     e.n_out = (uint32_t)(m - 1);
   }
-  launch_ntt(d_abc, L, true, D->lv_inv.as<uint32_t>(), D->icoset_lo.as<uint32_t>(), D->icoset_hi.as<uint32_t>(),
-             D->lo_bits, st, nullptr, e);
+  launch_ntt(d_abc, L, true, D->lv_inv.as<uint32_t>(), nullptr, D->icoset_full.as<uint32_t>(), POW_FULL_TABLE, st,
+             nullptr, e);
   BH_TRY_HIP(hipGetLastError());
   return BH_OK;
 }

@@ -68,6 +68,9 @@ struct Domain {
                                           // input (R = 2^256) read as device values (R = 2^261)
   DevBuf icoset_lo, icoset_hi;            // g^-i split, hi folded with m^-1        (icoset)
   DevBuf gpow_lo, gpow_hi;                // g^i (no m^-1)                           (coset_fft input)
+  // the H block's post-scale factors as full m-entry tables (coset, coset x 32, icoset: 36 B per
+  // entry, 453 MB at 2^22): one product per element in the storing pass instead of two
+  DevBuf coset_full, coset32_full, icoset_full;
   DevBuf consts;                          // [0] m^-1, [1] 1/Z(g), [2] one
   int lo_bits = 0;
   Fr minv, zinv;

@@ -17,8 +17,8 @@ struct DistArgs {
   uint32_t M, C, rank, m_minus_1;
   const uint32_t* tw_fwd;  // omega^j, j < m/2 (domain of size m, unpacked)
   const uint32_t* tw_inv;
-  const uint32_t* sc_lo;   // split power table over the global index k (g^k m^-1 or g^-k m^-1)
-  const uint32_t* sc_hi;
+  const uint32_t* sc_lo;   // power table over the global index k (g^k m^-1 or g^-k m^-1): split, or
+  const uint32_t* sc_hi;   // full in sc_hi (sc_bits = POW_FULL_TABLE, pow_factor)
   int sc_bits;
   uint32_t wN[16][9], wNinv[16][9];  // w_N^k, w_N^-k (device Montgomery limbs)
 };
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_dist_final(const uint32_t* recv, uint32
   for (int t = 0; t < N; t++) {
     const uint32_t k = t * a.M + q;
     DFr v = fe_mul<FrCfg>(x[t], pow_factor(a.sc_lo, a.sc_hi, a.sc_bits, k));
-    v = fe_reduce_full<FrCfg>(fe_mul<FrCfg>(v, one_raw));
+    v = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(v, one_raw));  // <= r: one subtraction
     uint32_t w[8];
     fe_pack<FrCfg>(v, w);
     uint4* p = reinterpret_cast<uint4*>(hbuf + ((size_t)t * a.C + u) * 8);
@@ -175,9 +175,10 @@ static bh_status make_args(bh_ctx* ctx, const DistH& d, bool icoset, DistArgs* a
   a->m_minus_1 = (uint32_t)(((size_t)1 << d.L) - 1);
   a->tw_fwd = D->tw_fwd.as<uint32_t>();
   a->tw_inv = D->tw_inv.as<uint32_t>();
-  a->sc_lo = icoset ? D->icoset_lo.as<uint32_t>() : D->coset_lo.as<uint32_t>();
-  a->sc_hi = icoset ? D->icoset_hi.as<uint32_t>() : D->coset_hi.as<uint32_t>();
-  a->sc_bits = D->lo_bits;
+  // the factors g^(+-k) m^-1 over the global index k: the domain's full tables (one load per element)
+  a->sc_lo = nullptr;
+  a->sc_hi = icoset ? D->icoset_full.as<uint32_t>() : D->coset_full.as<uint32_t>();
+  a->sc_bits = POW_FULL_TABLE;
   // w_N = root_of_unity^(2^(32 - log N))  (the same root as domain.rs:62-66, of order N)
   uint64_t rou_raw[4] = {0x3829971f439f0d2bull, 0xb63683508c2280b9ull, 0xd09b681922c813b4ull, 0x16a2a19edfe81f20ull};
   Fr w = from_int<4>(rou_raw);

@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) k_scalars_prepare(const uint32_t* in, uin
     DFr x = fe_unpack<FrCfg>(w);
     DFr k = fe_zero<FrCfg>();
     k.v[0] = (mode == 1) ? 32u : 1u;  // x*32*2^-261 = x*2^-256 ; x*2^-261
-    DFr r = fe_reduce_full<FrCfg>(fe_mul<FrCfg>(x, k));
+    DFr r = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(x, k));  // a product is < 2r: one subtraction
     fe_pack<FrCfg>(r, w);
   }
   uint4* q = reinterpret_cast<uint4*>(out + i * 8);

@@ -8,6 +8,9 @@
 
 namespace bh {
 
+constexpr int POW_FULL_TABLE = -2;
+  // post_lo_bits / pow_factor: a full m-entry table in hi
+
 struct FrConst {
   uint32_t v[9];  // raw 29-bit limbs
 };
@@ -32,7 +35,8 @@ struct NttEpilogue {
 // (default: d, in place).  dif=true: natural -> bit-reversed; dif=false: bit-reversed -> natural.
 // lv: per-level twiddles (9 limbs each) lv[2^v + x] = omega_{2^(v+1)}^x (launch_level_table).
 // post_lo/hi (optional): the stored element with natural index i is multiplied by
-// lo[i & mask] * hi[i >> lo_bits].
+// lo[i & mask] * hi[i >> lo_bits], or by hi[i] with post_lo_bits = POW_FULL_TABLE (one product
+// per element instead of two; the H block's coset / icoset factors, Domain::*_full).
 void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t* post_lo, const uint32_t* post_hi,
                 int post_lo_bits, hipStream_t st, const uint32_t* src = nullptr,
                 const NttEpilogue& epi = NttEpilogue());

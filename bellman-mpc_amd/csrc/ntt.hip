@@ -84,6 +84,26 @@ __device__ __forceinline__ DFr lw_norm(const DFr& a) {
   return r;
 }
 
+// x < 2^261 with normalised limbs below the top one -> x - q*r < 2r, one pass instead of a chain
+// of conditional subtractions (fe_csub 16, 8, 4, 2: ~40 VALU each).  r = r8 * 2^232 + r_low with
+// 0 < r_low < 2^232 and x < (x8 + 1) * 2^232, so q = floor(x8 / (r8 + 1)) gives q*r <= x and
+// x - q*r < (r8 + 1 + q) * 2^232 < 2r (q < 2^29 / r8 = 70).  The quotient comes from one FP64
+// fma, exact: (x8 + 1/2) / (r8 + 1) is at least 1/(2(r8 + 1)) ~ 6.6e-8 away from an integer,
+// far beyond the product's rounding (< 71 * 2^-52).
+__device__ __forceinline__ DFr fr_qreduce(const DFr& x) {
+  constexpr double inv = 1.0 / (double)(FrCfg::P[8] + 1u);
+  const uint32_t q = (uint32_t)__builtin_fma((double)x.v[8], inv, 0.5 * inv);
+  DFr r;
+  int64_t c = 0;
+#pragma unroll
+  for (int l = 0; l < 9; l++) {
+    const int64_t t = (int64_t)x.v[l] + c - (int64_t)((uint64_t)q * FrCfg::P[l]);
+    r.v[l] = l < 8 ? ((uint32_t)t & FrCfg::MASK) : (uint32_t)t;
+    c = t >> FrCfg::BITS;  // arithmetic
+  }
+  return r;
+}
+
 // global element index of (group g, position k) for a DIF pass at stages t..t+D-1
 __device__ __forceinline__ uint32_t dif_index(const PassArgs& a, uint32_t g, uint32_t k) {
   const uint32_t s = 1u << (a.L - a.t - a.D);
@@ -196,11 +216,11 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
         const DFr s02 = lw_add(x[0], x[2]), s13 = lw_add(x[1], x[3]);  // < 4r, limbs < 2^30
         const DFr u2 = fe_mul<FrCfg>(lw_sub<4, 1>(x[0], x[2]), wa0);   // < 2r
         const DFr u3 = fe_mul<FrCfg>(lw_sub<4, 1>(x[1], x[3]), wa1);
-        y[0] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(fe_add<FrCfg>(s02, s13)));  // < 8r
-        y[2] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u2, u3));                       // < 4r
+        y[0] = fr_qreduce(fe_add<FrCfg>(s02, s13));                  // < 8r
+        y[2] = fe_csub<FrCfg, 2>(fe_add<FrCfg>(u2, u3));                // < 4r
         if (v2 == 0) {  // omega_2^0 = 1
-          y[1] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(fe_csub<FrCfg, 8>(lw_norm(lw_sub<8, 2>(s02, s13)))));  // < 12r
-          y[3] = fe_csub<FrCfg, 2>(fe_csub<FrCfg, 4>(lw_norm(lw_sub<4, 1>(u2, u3))));  // < 6r
+          y[1] = fr_qreduce(lw_norm(lw_sub<8, 2>(s02, s13)));           // < 12r
+          y[3] = fr_qreduce(lw_norm(lw_sub<4, 1>(u2, u3)));             // < 6r
         } else {
           const DFr wb = twiddle(v2, ks[0] & m2, g);
           y[1] = fe_mul<FrCfg>(lw_sub<8, 2>(s02, s13), wb);  // operand < 12r, limbs < 2^31.4
@@ -267,18 +287,13 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
         DFr one = fe_zero<FrCfg>();
         one.v[0] = 1u;  // x * 1 * 2^-261: out of device Montgomery form
         uint32_t w8[8];
-        fe_pack<FrCfg>(fe_reduce_full<FrCfg>(fe_mul<FrCfg>(x, one)), w8);
+        fe_pack<FrCfg>(fe_csub<FrCfg, 1>(fe_mul<FrCfg>(x, one)), w8);  // (x * 1 + m r) / R <= r: one subtraction
         uint4* q = reinterpret_cast<uint4*>(a.epi.out + (size_t)nat * 8);
         q[0] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
         q[1] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
       }
     } else {
-      if (!DIF && !a.post_hi) {  // a lazily reduced DIT value (< 22r) -> < 2r for the packed form
-        x = fe_csub<FrCfg, 16>(x);
-        x = fe_csub<FrCfg, 8>(x);
-        x = fe_csub<FrCfg, 4>(x);
-        x = fe_csub<FrCfg, 2>(x);
-      }
+      if (!DIF && !a.post_hi) x = fr_qreduce(x);  // a lazily reduced DIT value (< 22r) -> < 2r for the packed form
       st_packed(data, idx, x);
     }
   }
@@ -355,7 +370,7 @@ __global__ void __launch_bounds__(256) k_fr_convert(const uint32_t* in, uint32_t
 #pragma unroll
   for (int l = 0; l < 9; l++) c.v[l] = C.v[l];
   DFr r = fe_mul<FrCfg>(x, c);
-  if (reduce) r = fe_reduce_full<FrCfg>(r);
+  if (reduce) r = fe_csub<FrCfg, 1>(r);  // a product is < 2r: one subtraction makes it canonical
   st_packed(out, i, r);
 }
 
@@ -396,9 +411,18 @@ void launch_ntt(uint32_t* d, int L, bool dif, const uint32_t* lv, const uint32_t
       scalars_prepare(d, epi.out, epi.n_out, 2, 0, st);
     return;
   }
+  // stages per pass: even where the total allows (a pass of odd depth runs one radix-2 stage,
+  // 330 instructions per butterfly against 293 in the radix-4 steps): 2^22 = 8 + 8 + 6, not 8 + 7 + 7
   const int passes = (L + 9) / 10;
   int Ds[8];
-  for (int p = 0; p < passes; p++) Ds[p] = L / passes + (p < L % passes ? 1 : 0);
+  const int pairs = L / 2;
+  for (int p = 0; p < passes; p++) Ds[p] = 2 * (pairs / passes + (p < pairs % passes ? 1 : 0));
+  if (L & 1) {  // one odd pass: the shallowest one takes the extra stage
+    int q = passes - 1;
+    for (int p = passes - 1; p >= 0; p--)
+      if (Ds[p] < Ds[q]) q = p;
+    Ds[q] += 1;
+  }
   int t = 0;
   for (int p = 0; p < passes; p++) {
     PassArgs a;

@@ -3,6 +3,7 @@
 // split power tables factor(i) = lo[i & mask] * hi[i >> lo_bits].
 #pragma once
 #include "field.cuh"
+#include "ntt.h"
 
 namespace bh {
 
@@ -29,8 +30,9 @@ __device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
   return bits ? (__builtin_bitreverse32(x) >> (32 - bits)) : 0u;
 }
 // factor(i) = lo[i & (2^lo_bits-1)] * hi[i >> lo_bits]   (tables unpacked)
-// lo_bits < 0: constant factor hi[0]
+// lo_bits = POW_FULL_TABLE (ntt.h): hi[i] (a full table); other lo_bits < 0: constant factor hi[0]
 __device__ __forceinline__ DFr pow_factor(const uint32_t* lo, const uint32_t* hi, int lo_bits, uint32_t i) {
+  if (lo_bits == POW_FULL_TABLE) return ld_limbs(hi, i);
   if (lo_bits < 0) return ld_limbs(hi, 0);
   return fe_mul<FrCfg>(ld_limbs(lo, i & ((1u << lo_bits) - 1u)), ld_limbs(hi, i >> lo_bits));
 }
