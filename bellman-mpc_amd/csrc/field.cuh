@@ -61,17 +61,51 @@ BH_DEV Fe<C> fe_one() {  // Montgomery form of 1
   return r;
 }
 
+// One step of a column chain: acc + a*b as ONE v_mad_u64_u32 with acc as its addend.  Written as
+// plain C (acc += (uint64_t)a * b) the compiler's reassociation starts every column on a fresh
+// chain of products and adds the carried accumulator afterwards (one 64-bit add per column); as
+// an opaque instruction the column stays one chain seeded with the carry (the hazard recogniser
+// follows each with an s_nop 0, which is not VALU work, and the chain is latency-bound per wave).
+// Measured (profiles/r06_ab_mul_chain.txt): Fr (the NTT, 4 waves per SIMD) -16 VALU per butterfly,
+// 2^22 proof -0.2 ms; Fp (the accumulations, 2 waves per SIMD) 5 129 -> 4 745 VALU per G1 madd but
+// the proof +1.2 ms and N = 8 +1.2 ms -- the latency costs more than the merges.  So Fr only.
+template <class C>
+struct MulChain {
+  static constexpr bool value = C::N == 9;  // FrCfg
+};
+template <bool CH>
+BH_DEV void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+  if (CH) {
+    uint64_t r, sc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(sc) : "v"(a), "v"(b), "v"(acc));
+    acc = r;
+  } else {
+    acc += (uint64_t)a * b;
+  }
+}
+// ... times a modulus limb (a compile-time constant: an SGPR operand)
+template <bool CH>
+BH_DEV void mac_p(uint64_t& acc, uint32_t m, uint32_t p) {
+  if (CH) {
+    uint64_t r, sc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(sc) : "v"(m), "s"(p), "v"(acc));
+    acc = r;
+  } else {
+    acc += (uint64_t)m * p;
+  }
+}
+
 // Montgomery product, FIPS column order. Output < 2p (see header).
 // A modulus with p = 1 (mod 2^BITS) (Fr) has m_k = -acc mod 2^BITS, so acc + m_k * p_0 is acc
 // rounded up to a multiple of 2^BITS: (acc + MASK) >> BITS, no product and no 64-bit m_k.
-// DFp keeps two independent chains (a*b and m*p) per column; for Fr the compiler splits the
-// column into a fresh chain plus a 64-bit merge either way (forcing one chain through inline
-// asm costs an s_nop per mad from the hazard recogniser).
+// DFp keeps two independent chains (a*b and m*p) per column, which the compiler schedules for
+// latency; Fr runs each column as one carry-seeded chain of opaque mads (MulChain, above).
 template <class C>
 BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
   constexpr int N = C::N;
   constexpr bool P0_ONE = C::P[0] == 1u;
-  constexpr bool TWO_CHAINS = N > 9;
+  constexpr bool CH = MulChain<C>::value;
+  constexpr bool TWO_CHAINS = N > 9 && !CH;
   Fe<C> r;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -79,12 +113,11 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
   for (int k = 0; k < 2 * N - 1; k++) {
     uint64_t acc2 = 0;
 #pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
-      acc += (uint64_t)a.v[i] * b.v[k - i];
+    for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) mac<CH>(acc, a.v[i], b.v[k - i]);
 #pragma unroll
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) {
       if (TWO_CHAINS) acc2 += (uint64_t)m[i] * C::P[k - i];
-      else acc += (uint64_t)m[i] * C::P[k - i];
+      else mac_p<CH>(acc, m[i], C::P[k - i]);
     }
     if (TWO_CHAINS) acc += acc2;
     if (k < N) {
@@ -93,7 +126,7 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
         acc = (acc + C::MASK) >> C::BITS;
         continue;
       }
-      acc += (uint64_t)m[k] * C::P[0];
+      mac_p<CH>(acc, m[k], C::P[0]);
     } else {
       r.v[k - N] = (uint32_t)acc & C::MASK;
     }
@@ -111,6 +144,7 @@ template <class C>
 BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>& d) {
   constexpr int N = C::N;
   static_assert(3 * N < 64, "3N products < 2^58 plus the carry must fit the 64-bit column accumulator");
+  constexpr bool CH = MulChain<C>::value;
   Fe<C> r;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -118,15 +152,14 @@ BH_DEV Fe<C> fe_mul2(const Fe<C>& a, const Fe<C>& b, const Fe<C>& c, const Fe<C>
   for (int k = 0; k < 2 * N - 1; k++) {
 #pragma unroll
     for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-      acc += (uint64_t)a.v[i] * b.v[k - i];
-      acc += (uint64_t)c.v[i] * d.v[k - i];
+      mac<CH>(acc, a.v[i], b.v[k - i]);
+      mac<CH>(acc, c.v[i], d.v[k - i]);
     }
 #pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
-      acc += (uint64_t)m[i] * C::P[k - i];
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) mac_p<CH>(acc, m[i], C::P[k - i]);
     if (k < N) {
       m[k] = ((uint32_t)acc * C::INV) & C::MASK;
-      acc += (uint64_t)m[k] * C::P[0];
+      mac_p<CH>(acc, m[k], C::P[0]);
     } else {
       r.v[k - N] = (uint32_t)acc & C::MASK;
     }
@@ -141,6 +174,7 @@ template <class C>
 BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
   constexpr int N = C::N;
   Fe<C> r;
+  constexpr bool CH = MulChain<C>::value;
   uint32_t m[N], a2[N];
 #pragma unroll
   for (int i = 0; i < N; i++) a2[i] = a.v[i] << 1;
@@ -152,15 +186,14 @@ BH_DEV Fe<C> fe_sqr(const Fe<C>& a) {
 #pragma unroll
     for (int i = lo; i <= hi; i++) {
       const int j = k - i;
-      if (i < j) acc += (uint64_t)a.v[i] * a2[j];
-      else if (i == j) acc += (uint64_t)a.v[i] * a.v[i];
+      if (i < j) mac<CH>(acc, a.v[i], a2[j]);
+      else if (i == j) mac<CH>(acc, a.v[i], a.v[i]);
     }
 #pragma unroll
-    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++)
-      acc += (uint64_t)m[i] * C::P[k - i];
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) mac_p<CH>(acc, m[i], C::P[k - i]);
     if (k < N) {
       m[k] = ((uint32_t)acc * C::INV) & C::MASK;
-      acc += (uint64_t)m[k] * C::P[0];
+      mac_p<CH>(acc, m[k], C::P[0]);
     } else {
       r.v[k - N] = (uint32_t)acc & C::MASK;
     }
