@@ -119,13 +119,11 @@ __global__ void __launch_bounds__(256) k_dist_final(const uint32_t* recv, uint32
   for (int r = 0; r < N; r++) x[r] = ld_packed(recv, u + (size_t)r * a.C);
   geometric<N>(x, ld_limbs(a.tw_inv, q));
   small_dft<N>(x, a.wNinv);
-  DFr one_raw = fe_zero<FrCfg>();
-  one_raw.v[0] = 1u;  // x * 1 * 2^-261: device Montgomery -> canonical
 #pragma unroll
   for (int t = 0; t < N; t++) {
     const uint32_t k = t * a.M + q;
     DFr v = fe_mul<FrCfg>(x[t], pow_factor(a.sc_lo, a.sc_hi, a.sc_bits, k));
-    v = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(v, one_raw));  // <= r: one subtraction
+    v = fe_csub<FrCfg, 1>(fe_from_mont<FrCfg>(v));  // <= r: one subtraction
     uint32_t w[8];
     fe_pack<FrCfg>(v, w);
     uint4* p = reinterpret_cast<uint4*>(hbuf + ((size_t)t * a.C + u) * 8);

@@ -136,6 +136,31 @@ BH_DEV Fe<C> fe_mul(const Fe<C>& a, const Fe<C>& b) {
   return r;
 }
 
+// x * R^-1 (fe_mul(x, 1) without the zero products): out of Montgomery form, <= p for x < R
+template <class C>
+BH_DEV Fe<C> fe_from_mont(const Fe<C>& a) {
+  constexpr int N = C::N;
+  constexpr bool CH = MulChain<C>::value;
+  Fe<C> r;
+  uint32_t m[N];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * N - 1; k++) {
+    if (k < N) acc += a.v[k];
+#pragma unroll
+    for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) mac_p<CH>(acc, m[i], C::P[k - i]);
+    if (k < N) {
+      m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+      mac_p<CH>(acc, m[k], C::P[0]);
+    } else {
+      r.v[k - N] = (uint32_t)acc & C::MASK;
+    }
+    acc >>= C::BITS;
+  }
+  r.v[N - 1] = (uint32_t)acc;
+  return r;
+}
+
 // (a*b + c*d) * R^-1 with ONE interleaved Montgomery reduction: every column absorbs the
 // products of both pairs and the m*p terms -- at most 3N = 42 products < 2^58 each for DFp,
 // so the 64-bit accumulator still needs no carry handling (2^63.4).  Output < 2p when the

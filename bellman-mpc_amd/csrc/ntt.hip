@@ -284,10 +284,8 @@ __global__ void __launch_bounds__(NTT_T) k_ntt_pass(uint32_t* data, PassArgs a) 
       st_packed(a.epi.pa, idx, fe_mul<FrCfg>(fe_sub<FrCfg, 32>(p, x), ld_limbs(a.epi.k, 0)));
     } else if (a.epi.kind == NttEpilogue::SCALARS) {  // canonical scalar at the natural index
       if (nat < a.epi.n_out) {
-        DFr one = fe_zero<FrCfg>();
-        one.v[0] = 1u;  // x * 1 * 2^-261: out of device Montgomery form
         uint32_t w8[8];
-        fe_pack<FrCfg>(fe_csub<FrCfg, 1>(fe_mul<FrCfg>(x, one)), w8);  // (x * 1 + m r) / R <= r: one subtraction
+        fe_pack<FrCfg>(fe_csub<FrCfg, 1>(fe_from_mont<FrCfg>(x)), w8);  // x * 2^-261 <= r: one subtraction
         uint4* q = reinterpret_cast<uint4*>(a.epi.out + (size_t)nat * 8);
         q[0] = make_uint4(w8[0], w8[1], w8[2], w8[3]);
         q[1] = make_uint4(w8[4], w8[5], w8[6], w8[7]);
