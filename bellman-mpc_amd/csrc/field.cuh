@@ -141,6 +141,7 @@ template <class C>
 BH_DEV Fe<C> fe_from_mont(const Fe<C>& a) {
   constexpr int N = C::N;
   constexpr bool CH = MulChain<C>::value;
+  constexpr bool P0_ONE = C::P[0] == 1u;
   Fe<C> r;
   uint32_t m[N];
   uint64_t acc = 0;
@@ -151,6 +152,10 @@ BH_DEV Fe<C> fe_from_mont(const Fe<C>& a) {
     for (int i = (k < N ? 0 : k - N + 1); i < (k < N ? k : N); i++) mac_p<CH>(acc, m[i], C::P[k - i]);
     if (k < N) {
       m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+      if (P0_ONE) {  // as in fe_mul
+        acc = (acc + C::MASK) >> C::BITS;
+        continue;
+      }
       mac_p<CH>(acc, m[k], C::P[0]);
     } else {
       r.v[k - N] = (uint32_t)acc & C::MASK;

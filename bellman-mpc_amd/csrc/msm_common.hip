@@ -137,9 +137,14 @@ __global__ void __launch_bounds__(256) k_scalars_prepare(const uint32_t* in, uin
     }
   } else {
     DFr x = fe_unpack<FrCfg>(w);
-    DFr k = fe_zero<FrCfg>();
-    k.v[0] = (mode == 1) ? 32u : 1u;  // x*32*2^-261 = x*2^-256 ; x*2^-261
-    DFr r = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(x, k));  // a product is < 2r: one subtraction
+    DFr r;
+    if (mode == 1) {
+      DFr k = fe_zero<FrCfg>();
+      k.v[0] = 32u;  // x*32*2^-261 = x*2^-256
+      r = fe_csub<FrCfg, 1>(fe_mul<FrCfg>(x, k));  // < r + 1: one subtraction
+    } else {
+      r = fe_csub<FrCfg, 1>(fe_from_mont<FrCfg>(x));  // x*2^-261 <= r
+    }
     fe_pack<FrCfg>(r, w);
   }
   uint4* q = reinterpret_cast<uint4*>(out + i * 8);
