@@ -1350,7 +1350,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // ~3x a G1 one) on the first accumulation's stream, every CU, right behind the G2 accumulation,
   // rather than on a quarter-CU tail stream: with three accumulation lanes the G1 accumulations end
   // earlier and at N = 8 that latency-bound tail (2.9 + 1.6 + 0.8 ms on 64 CUs) became the rank's
-  // critical path (gpurun_out/r6l trace).  Same-box A/B: the 2^22 bench 53.9-54.0 against 54.3-54.8
+  // critical path (profiles/r06_n8_rank0_timeline.txt).  Same-box A/B: the 2^22 bench 53.9-54.0 against 54.3-54.8
   // ms, bh_prove 57.9-58.2 against 58.4-58.9, rehearsal N = 1 / 2 / 8 at or below the base
   // (profiles/r06_ab_g2_tail.txt).  (On a pipelined batch lane the streams are shared: tail streams.)
   if (!serial && !ctx->borrowed_streams)
