@@ -1178,6 +1178,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   BH_TRY_HIP(hipEventRecord(jev[33], sS));
   if (!(up && up->on_vector)) BH_TRY_HIP(hipStreamWaitEvent(sH, jev[33], 0));
   int big[8], nbig = 0, small[8], nsmall = 0;
+  hipStream_t acc_stream[8] = {};  // the stream each large multiexp's accumulation was enqueued on
   for (int j = 0; j < 8; j++) {
     const size_t n = his[j] - los[j];
     if (!n || (host_in && j >= 5)) continue;
@@ -1275,6 +1276,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     hipStream_t s0 = first_own ? sT : sA;
     BH_TRY_HIP(hipStreamWaitEvent(s0, jev[16 + wait_j], 0));
     if ((s = acc_job(big[0], s0))) return s;
+    acc_stream[0] = s0;
   }
   // With the first accumulation on its own stream, the second one (G1: b_g1_aux, whose sorted
   // entries are a copy among the first sorts) is enqueued right behind it, before the remaining
@@ -1286,6 +1288,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
     for (int r = 0; r < pre_sorts; r++) pre = pre || sorder[r] == big[1];
     if (pre) {
       if ((s = acc_job(big[1], sA))) return s;
+      acc_stream[1] = sA;
       q_first = 2;
     }
   }
@@ -1329,6 +1332,7 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
       sq = l == 0 ? sT : l == 1 ? sA : ctx->stream5;
     }
     if ((s = acc_job(big[q], sq))) return s;
+    acc_stream[q] = sq;
   }
   if (!h_done && (s = enqueue_h(jev[33]))) return s;  // (no large h job: H still runs)
   if ((s = run_small())) return s;
@@ -1345,7 +1349,10 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   const auto t_hand = std::chrono::steady_clock::now();
   if (t_lane.after_accs) t_lane.after_accs();
   if (t_lane.before_tails) t_lane.before_tails();
-  if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = sT;
+  // The last tail right behind its own accumulation, on that lane (every CU): with three lanes
+  // (round 6) the first accumulation's stream may still be running the G2 tail below, which held
+  // the last tail back 0.9 ms at N = 8 (profiles/r06_n8_rank0_timeline.txt, second trace).
+  if (last_full && nbig > 0 && nsmall == 0) tails[nbig - 1] = multi_lane ? acc_stream[nbig - 1] : sT;
   // The G2 multiexp's reduction tail (continuation fold + reduction of G2 buckets, each addition
   // ~3x a G1 one) on the first accumulation's stream, every CU, right behind the G2 accumulation,
   // rather than on a quarter-CU tail stream: with three accumulation lanes the G1 accumulations end
@@ -1353,9 +1360,14 @@ bh_status compute_msms(bh_ctx* ctx, const bh_params* params, const bh_witness* w
   // critical path (profiles/r06_n8_rank0_timeline.txt).  Same-box A/B: the 2^22 bench 53.9-54.0 against 54.3-54.8
   // ms, bh_prove 57.9-58.2 against 58.4-58.9, rehearsal N = 1 / 2 / 8 at or below the base
   // (profiles/r06_ab_g2_tail.txt).  (On a pipelined batch lane the streams are shared: tail streams.)
+  // (only where no later accumulation queued on that stream: the tail would wait for it)
   if (!serial && !ctx->borrowed_streams)
-    for (int q = 0; q + 1 < nbig; q++)
-      if (jobs[big[q]].g2) tails[q] = sT;
+    for (int q = 0; q + 1 < nbig; q++) {
+      if (!jobs[big[q]].g2 || !acc_stream[q]) continue;
+      bool later = false;
+      for (int r = q + 1; r < nbig; r++) later = later || acc_stream[r] == acc_stream[q];
+      if (!later) tails[q] = acc_stream[q];
+    }
   for (int q = 0; q < nbig; q++) {
     if ((s = tail_job(big[q], tails[q]))) return s;
     BH_TRY_HIP(hipEventRecord(ctx->ev[2 + q], tails[q]));
